@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: NLSPN propagation iterations/s on MI355X (BASELINE.json metric).
+
+One "step" = the whole propagation section of NLSPNModel.forward
+(src/model/nlspnmodel.py:323-381) over one synthetic batch: the prologue
+(affinity normalisation, offset insertion, confidence/input blend) plus T fused
+iterations, replayed as one native hipGraph (nlspn_plan_launch).  Inputs are
+resident in HBM before the timed region.  value = iterations/s summed over all
+ranks = N * T * steps / max-over-ranks wall time.
+
+Default workload = BASELINE config C2 (configs[1]): NYUv2 228x304, K=8, T=18,
+B=8, fp32, learned offsets (DCN path), TGASS.  --config kitti = C3, nyu_k16 = C5.
+Multi-GPU (torchrun): every rank runs its own batch (weak scaling, no collective
+on the data path) — the all_reduce below only takes the max time.
+
+Extra JSON objects:
+  roofline     — the fused iteration kernel: algorithmic bytes per launch
+                 (S*(4+3K) per pixel) / mean kernel duration from
+                 dispatch-recorded HIP events (nlspn_time_prop_step) on this
+                 stream; traffic from profiles/pmc_<config>.json when present.
+  cpu_baseline — the C oracle (kind "port"; the reference has no CPU DCN path)
+                 on the same workload, rank 0, N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from nlspn_eccv20_amd import _lib  # noqa: E402
+from nlspn_eccv20_amd.propagation import PropagationPlan, _ptr, _stream  # noqa: E402
+from nlspn_eccv20_amd.sharding import max_over_ranks  # noqa: E402
+from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
+
+CONFIGS = {
+    "nyu": dict(id="C2", desc="NYUv2 228x304, K=8, T=18, B=8, fp32, learned offsets, TGASS",
+                B=8, H=228, W=304, kernel=(3, 3), T=18, dtype="f32", max_depth=10.0, density=500 / (228 * 304)),
+    "kitti": dict(id="C3", desc="KITTI-DC 240x1216, K=8, T=18, B=4, fp32, learned offsets, TGASS",
+                  B=4, H=240, W=1216, kernel=(3, 3), T=18, dtype="f32", max_depth=90.0, density=0.05),
+    "nyu_k16": dict(id="C5", desc="NYUv2 228x304, K=16 (1x17), T=36, B=16, fp16 storage, learned offsets, TGASS",
+                    B=16, H=228, W=304, kernel=(1, 17), T=36, dtype="f16", max_depth=10.0, density=500 / (228 * 304)),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def baseline_metric():
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except (OSError, KeyError, ValueError):
+        return "propagation iters/sec (+ ms/iter)"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="nyu", choices=sorted(CONFIGS))
+    ap.add_argument("--kernel-reps", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    return ap.parse_args()
+
+
+def kernel_time(plan, inputs, cfg, reps, dev):
+    """Mean/min duration of the fused iteration kernel from dispatch-recorded events."""
+    o = plan.outputs
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    off = inputs["off"]
+    p_out = torch.empty_like(o["pred"])
+    H, W, B = cfg["H"], cfg["W"], cfg["B"]
+    mean_ms, min_ms = ctypes.c_float(), ctypes.c_float()
+    dt = _lib.DTYPE_F16 if cfg["dtype"] == "f16" else _lib.DTYPE_F32
+    _lib.check(_lib.get().nlspn_time_prop_step(
+        dt, _ptr(o["pred_inter"][0]), _ptr(o["confidence"]), _ptr(inputs["dep"]), _ptr(o["aff"]),
+        (K + 1) * H * W, _ptr(off), off.stride(0), _lib.OFF_RAW, _ptr(p_out), B, H, W,
+        cfg["kernel"][0], cfg["kernel"][1], _lib.PRESERVE_INPUT, reps, _stream(dev),
+        ctypes.byref(mean_ms), ctypes.byref(min_ms)))
+    return mean_ms.value, min_ms.value
+
+
+def cpu_baseline(cfg, s, reps):
+    from oracle import oracle as O  # test infrastructure: the CPU baseline leg only
+    threads = max(1, min(16, os.cpu_count() or 1))
+    O.set_threads(threads)
+    K = s["K"]
+    args = (s["pred_init"], s["dep"], s["conf"], s["off_aff"][:, 2 * K:], s["off_aff"][:, :2 * K], 0.5 * K)
+    kw = dict(kh=cfg["kernel"][0], kw=cfg["kernel"][1], prop_time=cfg["T"])
+    O.propagate(*args, **kw)  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        O.propagate(*args, **kw)
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return {"value": cfg["T"] / med, "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/nlspn_oracle.c, OpenMP {threads} threads, fp32) on the full "
+                      f"{cfg['id']} batch, 1 warm-up + median of {reps} whole propagations of T={cfg['T']}",
+            "ms_per_iter": 1e3 * med / cfg["T"]}
+
+
+def main():
+    a = parse()
+    cfg = CONFIGS[a.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    tdt = torch.float16 if cfg["dtype"] == "f16" else torch.float32
+
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    s = synth(cfg["B"], cfg["H"], cfg["W"], K, seed=7240 + rank, density=cfg["density"],
+              max_depth=cfg["max_depth"])
+    to = lambda x: torch.from_numpy(x).to(dev, tdt)  # noqa: E731
+    off_aff = to(s["off_aff"])
+    inputs = {"pred_init": to(s["pred_init"]), "dep": to(s["dep"]), "conf": to(s["conf"]),
+              "aff": off_aff[:, 2 * K:], "off": off_aff[:, :2 * K],
+              "gamma": torch.tensor([0.5 * K], device=dev)}
+    plan = PropagationPlan(inputs["pred_init"], inputs["dep"], inputs["conf"], inputs["aff"], inputs["off"],
+                           inputs["gamma"], prop_time=cfg["T"], kernel=cfg["kernel"])
+    for _ in range(a.warmup):
+        plan.replay()
+    torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(a.steps):
+        plan.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    elapsed = max_over_ranks(elapsed, dev)
+
+    kmean, kmin = kernel_time(plan, inputs, cfg, a.kernel_reps, dev)
+    npx = cfg["B"] * cfg["H"] * cfg["W"]
+    es = 2 if cfg["dtype"] == "f16" else 4
+    bytes_per_launch = es * (4 + 3 * K) * npx
+    achieved = bytes_per_launch / (kmean * 1e-3) / 1e9
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    ms_per_step = 1e3 * elapsed / a.steps
+    value = world * cfg["T"] * a.steps / elapsed
+    out = {
+        "metric": baseline_metric(),
+        "value": round(value, 1), "unit": "iters/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4), "ms_per_iter": round(ms_per_step / cfg["T"], 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
+        "data": "synthetic (seeded; SURVEY §8d distribution, convex |N(0,1)| affinity, N(0,2^2) offsets)",
+        "config": {"workload": f"{cfg['id']}: {cfg['desc']}", "batch_per_gpu": cfg["B"],
+                   "global_batch": cfg["B"] * world, "H": cfg["H"], "W": cfg["W"], "K": K,
+                   "kernel": list(cfg["kernel"]), "prop_time": cfg["T"],
+                   "parallelism": f"dp{world} (batch shards, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "prop_step_kernel (one fused iteration)",
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "kernel_ms_mean": round(kmean, 5), "kernel_ms_min": round(kmin, 5)},
+        "gpu_event_ms_per_step": round(gpu_ms / a.steps, 4),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, s, a.cpu_reps)
+    plan.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

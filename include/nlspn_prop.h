@@ -1,0 +1,174 @@
+/*
+ * nlspn_prop.h — C ABI of the MI355X-native NLSPN propagation hot path.
+ *
+ * Drop-in boundary for XJTUXYC/NLSPN_ECCV20's non-local spatial propagation
+ * (src/model/nlspnmodel.py:179-381) and the DCNv2 forward it rides on
+ * (src/model/deformconv/src/vision.cpp:9 -> modulated_deform_conv.h:10-44 ->
+ *  cuda/modulated_deform_conv_cuda.cu:19-121).  Plain pointers and sizes only:
+ * no torch types cross this boundary.  All device pointers are caller-owned
+ * (allocated by the caller on the current device); nothing is allocated on the
+ * hot path.  `stream` is a hipStream_t passed as void* (NULL = legacy default
+ * stream).  Every call only enqueues work; none synchronises the host, so every
+ * call may be captured into a hipGraph.
+ *
+ * Layout: NCHW with one channel per plane; a "plane" is H*W contiguous
+ * elements; tensors with several planes per batch item take a batch stride in
+ * ELEMENTS (so slices of a (B,3K,H,W) off_aff head output can be passed without
+ * a copy, as nlspnmodel.py:304-305 slices it).
+ *
+ * Errors: functions return 0 on success, a positive NLSPN_E* code otherwise;
+ * nlspn_last_error() gives the message (thread-local), worded like the
+ * reference's AT_ASSERTM/AT_ERROR messages where one exists.
+ */
+#ifndef NLSPN_PROP_H
+#define NLSPN_PROP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLSPN_ABI_VERSION 1
+
+/* element type of every tensor argument (math is always fp32) */
+#define NLSPN_DTYPE_F32 0
+#define NLSPN_DTYPE_F16 1
+
+/* affinity normalisation kinds, src/config.py:259-263 / nlspnmodel.py:179-201 */
+#define NLSPN_AFF_AS 0
+#define NLSPN_AFF_ASS 1
+#define NLSPN_AFF_TC 2
+#define NLSPN_AFF_TGASS 3
+
+/* flags (bit set) — src/config.py:250-257 */
+#define NLSPN_PRESERVE_INPUT 0x1u /* args.preserve_input, nlspnmodel.py:328-334,342-344,355-357 */
+#define NLSPN_ALWAYS_CLIP 0x2u    /* args.always_clip,    nlspnmodel.py:346-348,359-361,375-377 */
+
+/* offset plane layout for nlspn_prop_step */
+#define NLSPN_OFF_INSERTED 0 /* (B, 2(K+1), H, W): tap t uses planes 2t (dh), 2t+1 (dw) — _off_insert output */
+#define NLSPN_OFF_RAW 1      /* (B, 2K, H, W): the head's raw slice; the reference tap is implicit zero */
+
+/* error codes */
+#define NLSPN_OK 0
+#define NLSPN_EINVAL 1       /* bad shape / argument */
+#define NLSPN_EUNSUPPORTED 2 /* geometry or dtype without a kernel instantiation */
+#define NLSPN_EHIP 3         /* HIP runtime / launch error */
+
+/* Version of this ABI (NLSPN_ABI_VERSION). */
+int nlspn_abi_version(void);
+
+/* Message for the last error on this thread ("" if none). */
+const char *nlspn_last_error(void);
+
+/*
+ * Affinity normalisation + reference-tap insertion.
+ * Replaces NLSPNModel._affinity_normalization (src/model/nlspnmodel.py:179-201)
+ * followed by _aff_insert (:261-269).
+ *   aff_raw : B x K planes, batch stride aff_bstride
+ *   gamma   : device pointer to ONE float32 (aff_scale_const, :93-104); read on
+ *             the device so a graph replay sees the current value (learnable γ)
+ *   aff_out : B x (K+1) planes, contiguous, reference tap at index K/2
+ */
+int nlspn_affinity_normalize(int dtype, const void *aff_raw, int64_t aff_bstride,
+                             const float *gamma, void *aff_out,
+                             int B, int K, int H, int W, int kind, void *stream);
+
+/*
+ * One fused propagation iteration: f = p_in * conf (conf may be NULL,
+ * nlspnmodel.py:350-353), out = _propagate_once(f, offset, aff) (:203-226),
+ * then the preserve-input blend (:355-357) and clamp (:359-361) per flags.
+ * Replaces, per iteration, DCN.modulated_deform_conv_forward
+ * (modulated_deform_conv_func.py:26; vision.cpp:9; .cu:19-121) with NLSPN's
+ * all-ones 1x1xkhxkw weight and zero bias, plus ~5 elementwise torch ops.
+ *   p_in, conf, dep : B planes (contiguous); dep may be NULL without PRESERVE
+ *   aff     : normalised affinity, B x (K+1) planes, batch stride aff_bstride
+ *             (the tap at K/2 is NOT read: it is recomputed as 1 - sum of the
+ *             others, bit-identical to what nlspn_affinity_normalize wrote)
+ *   off     : offsets, batch stride off_bstride, layout NLSPN_OFF_* (NULL ->
+ *             the no-offset branch :209-224: 3x3 replicate padding, K must be 8)
+ *   p_out   : B planes; pred_out (optional): max(out, 0) — the epilogue :375-377
+ *   kh, kw  : DCN kernel geometry (odd; K = kh*kw - 1). 3x3 = prop_kernel 3.
+ */
+int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *dep,
+                    const void *aff, int64_t aff_bstride,
+                    const void *off, int64_t off_bstride, int off_layout,
+                    void *p_out, void *pred_out,
+                    int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
+
+/* Bytes of device workspace nlspn_propagate needs (one plane per batch item). */
+size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
+
+/*
+ * The whole propagation section, src/model/nlspnmodel.py:323-381, as
+ * 1 prologue launch + T iteration launches:
+ *   prologue : _off_insert (:324) if off_out, _affinity_normalization (:325),
+ *              mask_fix / confidence blend (:328-334), first blend+clamp (:341-348)
+ *   T steps  : nlspn_prop_step, writing pred_inter[t]; the last also writes pred.
+ * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
+ *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
+ *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
+ * Outputs: pred_inter (T x B planes, contiguous: list_pred), pred (B planes),
+ *          aff_out (B x (K+1) planes), off_out (B x 2(K+1) planes, optional),
+ *          conf_out (B planes, required iff conf != NULL).
+ * workspace: nlspn_workspace_bytes() bytes of device memory.
+ */
+int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
+                    const void *aff_raw, int64_t aff_bstride,
+                    const void *off_raw, int64_t off_bstride, const float *gamma,
+                    void *pred_inter, void *pred, void *aff_out, void *off_out,
+                    void *conf_out, void *workspace,
+                    int B, int H, int W, int kh, int kw, int T, int kind,
+                    unsigned flags, void *stream);
+
+/*
+ * Graph plans: nlspn_propagate captured once into a hipGraph (1 + T kernel
+ * nodes) and replayed with one hipGraphLaunch.  Pointers are baked in at
+ * creation; γ stays live because it is read from device memory.
+ */
+typedef struct nlspn_plan *nlspn_plan_t;
+int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep,
+                      const void *conf, const void *aff_raw, int64_t aff_bstride,
+                      const void *off_raw, int64_t off_bstride, const float *gamma,
+                      void *pred_inter, void *pred, void *aff_out, void *off_out,
+                      void *conf_out, void *workspace,
+                      int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags);
+int nlspn_plan_launch(nlspn_plan_t plan, void *stream);
+int nlspn_plan_destroy(nlspn_plan_t plan);
+
+/*
+ * Modulated DCNv2 forward, seam 2 of the drop-in (the `DCN` pybind module,
+ * src/model/deformconv/src/vision.cpp:9, modulated_deform_conv.h:10-44,
+ * cuda/modulated_deform_conv_cuda.cu:19-121), as one direct (GEMM-free) gather
+ * kernel.  All tensors contiguous NCHW.
+ *   input (B,C,H,W), weight (Cout, C/group, kh, kw), bias (Cout) or NULL,
+ *   offset (B, 2*dg*kh*kw, Ho, Wo), mask (B, dg*kh*kw, Ho, Wo),
+ *   output (B, Cout, Ho, Wo) with Ho = (H + 2ph - (dh(kh-1)+1))/sh + 1 (.cu:75-76).
+ * Unlike the reference there is no im2col_step batch-divisibility restriction
+ * (.cu:58-60); im2col_step is accepted and ignored.
+ */
+int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const void *bias,
+                       const void *offset, const void *mask, void *output,
+                       int B, int C, int H, int W, int Cout, int kh, int kw,
+                       int sh, int sw, int ph, int pw, int dh, int dw,
+                       int group, int deformable_group, void *stream);
+
+/*
+ * Diagnostics (not part of the reference surface): enqueue `reps` back-to-back
+ * nlspn_prop_step launches on `stream`, each bracketed by its own HIP event
+ * pair recorded by the dispatch itself (hipExtLaunchKernelGGL start/stop
+ * events), then synchronise and return the mean and min per-launch kernel
+ * duration in ms.  Used by bench.py for the roofline's kernel time.
+ */
+int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const void *dep,
+                         const void *aff, int64_t aff_bstride,
+                         const void *off, int64_t off_bstride, int off_layout,
+                         void *p_out, int B, int H, int W, int kh, int kw, unsigned flags,
+                         int reps, void *stream, float *mean_ms, float *min_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NLSPN_PROP_H */

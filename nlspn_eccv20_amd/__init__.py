@@ -1,0 +1,17 @@
+"""nlspn_eccv20_amd — MI355X-native (gfx950) NLSPN non-local spatial propagation.
+
+The hot path of XJTUXYC/NLSPN_ECCV20 (src/model/nlspnmodel.py:179-381 and the DCNv2
+forward it calls) as hand-written HIP kernels behind a C ABI (include/nlspn_prop.h),
+with a torch-facing mirror of the reference interface:
+
+  propagation.affinity_normalization / off_insert / prop_step / propagate
+  propagation.PropagationPlan   — the whole section as one native hipGraph
+  propagation.NLSPNPropagation  — nn.Module with the reference's state_dict names
+  dcn                           — `DCN`-compatible module (seam 2)
+"""
+from .propagation import (NLSPNPropagation, PropagationPlan, affinity_normalization, kernel_geometry,
+                          off_insert, prop_step, propagate)
+
+__all__ = ["NLSPNPropagation", "PropagationPlan", "affinity_normalization", "kernel_geometry", "off_insert",
+           "prop_step", "propagate"]
+__version__ = "0.1.0"

@@ -1,0 +1,403 @@
+// C ABI of the NLSPN propagation hot path (see include/nlspn_prop.h).
+// Host side: argument validation with reference-style messages, kernel
+// instantiation dispatch, the T-iteration launch sequence, hipGraph plans and
+// the dispatch-event timing helper used by bench.py.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/nlspn_prop.h"
+#include "nlspn_mdcn.h"
+#include "nlspn_prologue.h"
+#include "nlspn_step.h"
+
+using namespace nlspn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define NLSPN_HIP_TRY(expr)                                                               \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail(NLSPN_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+inline int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(NLSPN_EHIP, "error in %s: %s", what, hipGetErrorString(e));
+    return NLSPN_OK;
+}
+
+inline size_t esize(int dtype) { return dtype == NLSPN_DTYPE_F16 ? 2 : 4; }
+
+inline bool aligned(const void *p, size_t a) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- step dispatch
+struct StepLaunch {
+    const void *fn = nullptr;  // kernel address
+    dim3 grid, block;
+};
+
+template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE>
+StepLaunch make_step(StepArgs &a) {
+    StepLaunch L;
+    L.fn = reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, OFFSET, PRE>);
+    a.tiles_x = (a.W + TW - 1) / TW;
+    a.tiles_y = (a.H + TH - 1) / TH;
+    L.grid = dim3((unsigned)(a.B * a.tiles_x * a.tiles_y));
+    L.block = dim3(TH * TW / PX);
+    return L;
+}
+
+// Tile configurations per geometry.  vec: 16-B (fp32) / 8-B (fp16) lane loads,
+// needs W % 4 == 0 and aligned planes; scalar: any shape.
+template <typename T>
+int select_step(StepArgs &a, int kh, int kw, bool offset, bool vec, StepLaunch &L) {
+    if (!offset) {
+        if (kh != 3 || kw != 3)
+            return fail(NLSPN_EUNSUPPORTED,
+                        "no-offset propagation is 3x3 replicate (nlspnmodel.py:209-224); got %dx%d", kh, kw);
+        L = vec ? make_step<T, 3, 3, 16, 64, 4, 1, 1, 1, false, false>(a)
+                : make_step<T, 3, 3, 4, 64, 1, 1, 1, 1, false, false>(a);
+        return NLSPN_OK;
+    }
+    if (kh == 3 && kw == 3)
+        L = vec ? make_step<T, 3, 3, 16, 64, 4, 8, 8, 4, true, true>(a)
+                : make_step<T, 3, 3, 4, 64, 1, 8, 8, 1, true, true>(a);
+    else if (kh == 1 && kw == 17)
+        L = vec ? make_step<T, 1, 17, 16, 64, 4, 8, 16, 4, true, false>(a)
+                : make_step<T, 1, 17, 4, 64, 1, 8, 16, 1, true, false>(a);
+    else if (kh == 5 && kw == 5)
+        L = vec ? make_step<T, 5, 5, 8, 64, 2, 8, 8, 4, true, false>(a)
+                : make_step<T, 5, 5, 4, 64, 1, 8, 8, 1, true, false>(a);
+    else if (kh == 7 && kw == 7)
+        L = vec ? make_step<T, 7, 7, 8, 64, 2, 8, 8, 4, true, false>(a)
+                : make_step<T, 7, 7, 4, 64, 1, 8, 8, 1, true, false>(a);
+    else
+        return fail(NLSPN_EUNSUPPORTED, "no kernel instantiation for a %dx%d propagation geometry "
+                    "(supported: 3x3, 5x5, 7x7, 1x17)", kh, kw);
+    return NLSPN_OK;
+}
+
+struct StepReq {
+    int dtype;
+    StepArgs a;
+    int kh, kw;
+};
+
+int prepare_step(StepReq &r, StepLaunch &L) {
+    StepArgs &a = r.a;
+    if (r.dtype != NLSPN_DTYPE_F32 && r.dtype != NLSPN_DTYPE_F16)
+        return fail(NLSPN_EUNSUPPORTED, "dtype %d not supported (f32=0, f16=1)", r.dtype);
+    if (a.B < 1 || a.H < 1 || a.W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", a.B, a.H, a.W);
+    if (r.kh < 1 || r.kw < 1 || (r.kh % 2) == 0 || (r.kw % 2) == 0 || r.kh * r.kw < 2)
+        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", r.kh, r.kw);
+    if (!a.p_in || !a.aff || !a.p_out) return fail(NLSPN_EINVAL, "p_in, aff and p_out must be non-null");
+    if ((a.flags & kPreserve) && !a.dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    const long long HW = (long long)a.H * a.W;
+    const int K = r.kh * r.kw - 1;
+    if (a.aff_bs < (long long)(K + 1) * HW) return fail(NLSPN_EINVAL, "aff batch stride %lld < (K+1)*H*W", a.aff_bs);
+    if (a.off) {
+        const long long need = (long long)(a.off_raw ? 2 * K : 2 * (K + 1)) * HW;
+        if (a.off_bs < need) return fail(NLSPN_EINVAL, "offset batch stride %lld < %lld", a.off_bs, need);
+    }
+    if ((long long)a.B * ((a.H + 3) / 4) * ((a.W + 63) / 64) > 0x7fffffffLL)
+        return fail(NLSPN_EINVAL, "grid too large");
+    const size_t vb = 4 * esize(r.dtype);
+    const bool vec = (a.W % 4 == 0) && (a.aff_bs % 4 == 0) && (!a.off || a.off_bs % 4 == 0) &&
+                     aligned(a.p_in, vb) && aligned(a.conf, vb) && aligned(a.dep, vb) && aligned(a.aff, vb) &&
+                     aligned(a.off, vb) && aligned(a.p_out, vb) && aligned(a.pred_out, vb);
+    return r.dtype == NLSPN_DTYPE_F32 ? select_step<float>(a, r.kh, r.kw, a.off != nullptr, vec, L)
+                                      : select_step<__half>(a, r.kh, r.kw, a.off != nullptr, vec, L);
+}
+
+int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    void *args[] = {&a};
+    if (e0)
+        NLSPN_HIP_TRY(hipExtLaunchKernel(L.fn, L.grid, L.block, args, 0, s, e0, e1, 0));
+    else
+        NLSPN_HIP_TRY(hipLaunchKernel(L.fn, L.grid, L.block, args, 0, s));
+    return check_launch("nlspn_prop_step");
+}
+
+// ------------------------------------------------------------ prologue dispatch
+template <typename T, int K>
+const void *prologue_fn(bool vec) {
+    return vec ? reinterpret_cast<const void *>(&prologue_kernel<T, K, 4>)
+               : reinterpret_cast<const void *>(&prologue_kernel<T, K, 1>);
+}
+template <typename T>
+const void *select_prologue(int K, bool vec) {
+    switch (K) {
+        case 8: return prologue_fn<T, 8>(vec);
+        case 16: return prologue_fn<T, 16>(vec);
+        case 24: return prologue_fn<T, 24>(vec);
+        case 48: return prologue_fn<T, 48>(vec);
+        default: return nullptr;
+    }
+}
+template <typename T, int K>
+const void *affnorm_fn(bool vec) {
+    return vec ? reinterpret_cast<const void *>(&affnorm_kernel<T, K, 4>)
+               : reinterpret_cast<const void *>(&affnorm_kernel<T, K, 1>);
+}
+template <typename T>
+const void *select_affnorm(int K, bool vec) {
+    switch (K) {
+        case 8: return affnorm_fn<T, 8>(vec);
+        case 16: return affnorm_fn<T, 16>(vec);
+        case 24: return affnorm_fn<T, 24>(vec);
+        case 48: return affnorm_fn<T, 48>(vec);
+        default: return nullptr;
+    }
+}
+
+unsigned elementwise_grid(long long groups) {
+    long long g = (groups + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nlspn_abi_version(void) { return NLSPN_ABI_VERSION; }
+
+const char *nlspn_last_error(void) { return g_err.c_str(); }
+
+int nlspn_affinity_normalize(int dtype, const void *aff_raw, int64_t aff_bstride, const float *gamma,
+                             void *aff_out, int B, int K, int H, int W, int kind, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    if (!aff_raw || !gamma || !aff_out) return fail(NLSPN_EINVAL, "null pointer");
+    const long long HW = (long long)H * W;
+    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
+    const size_t vb = 4 * esize(dtype);
+    const bool vec = HW % 4 == 0 && aff_bstride % 4 == 0 && aligned(aff_raw, vb) && aligned(aff_out, vb);
+    const void *fn = dtype == NLSPN_DTYPE_F32 ? select_affnorm<float>(K, vec) : select_affnorm<__half>(K, vec);
+    if (!fn) return fail(NLSPN_EUNSUPPORTED, "no affinity kernel for K=%d (supported 8, 16, 24, 48)", K);
+    long long bs = aff_bstride, hw = HW;
+    int b = B, k = kind;
+    void *args[] = {(void *)&aff_raw, &bs, (void *)&gamma, &aff_out, &hw, &b, &k};
+    NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(elementwise_grid((long long)B * HW / (vec ? 4 : 1))), dim3(256), args, 0,
+                                  as_stream(stream)));
+    return check_launch("nlspn_affinity_normalize");
+}
+
+int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *dep, const void *aff,
+                    int64_t aff_bstride, const void *off, int64_t off_bstride, int off_layout, void *p_out,
+                    void *pred_out, int B, int H, int W, int kh, int kw, unsigned flags, void *stream) {
+    StepReq r{};
+    r.dtype = dtype;
+    r.kh = kh;
+    r.kw = kw;
+    r.a = StepArgs{p_in, conf, dep, aff, off, p_out, pred_out, aff_bstride, off_bstride, B, H, W, 0, 0,
+                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags};
+    StepLaunch L;
+    int rc = prepare_step(r, L);
+    if (rc) return rc;
+    return launch(L, r.a, as_stream(stream));
+}
+
+size_t nlspn_workspace_bytes(int dtype, int B, int H, int W) { return esize(dtype) * (size_t)B * H * W; }
+
+int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
+                    int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
+                    void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out, void *workspace,
+                    int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
+        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
+    if (!pred_init || !aff_raw || !gamma || !pred_inter || !pred || !aff_out || !workspace)
+        return fail(NLSPN_EINVAL, "null required pointer");
+    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    if (conf && !conf_out) return fail(NLSPN_EINVAL, "conf given without conf_out");
+    if (off_out && !off_raw) return fail(NLSPN_EINVAL, "off_out given without off_raw");
+    const int K = kh * kw - 1;
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
+    if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
+    hipStream_t s = as_stream(stream);
+    const size_t es = esize(dtype);
+
+    // validate the step configuration before launching anything
+    StepReq r{};
+    r.dtype = dtype;
+    r.kh = kh;
+    r.kw = kw;
+    r.a = StepArgs{workspace, conf ? conf_out : nullptr, dep, aff_out, off_raw, pred_inter, pred,
+                   (long long)(K + 1) * HW, off_bstride, B, H, W, 0, 0, 1, flags};
+    StepLaunch L;
+    int rc = prepare_step(r, L);
+    if (rc) return rc;
+
+    // prologue
+    const size_t vb = 4 * es;
+    const bool pvec = HW % 4 == 0 && aff_bstride % 4 == 0 && (!off_raw || off_bstride % 4 == 0) &&
+                      aligned(pred_init, vb) && aligned(dep, vb) && aligned(conf, vb) && aligned(aff_raw, vb) &&
+                      aligned(off_raw, vb) && aligned(aff_out, vb) && aligned(off_out, vb) && aligned(conf_out, vb) &&
+                      aligned(workspace, vb);
+    const void *pfn = dtype == NLSPN_DTYPE_F32 ? select_prologue<float>(K, pvec) : select_prologue<__half>(K, pvec);
+    if (!pfn) return fail(NLSPN_EUNSUPPORTED, "no prologue kernel for K=%d (supported 8, 16, 24, 48)", K);
+    PrologueArgs pa{pred_init, dep, conf, aff_raw, off_raw, gamma, aff_out, off_out, conf_out, workspace,
+                    aff_bstride, off_bstride, HW, B, kind, flags};
+    void *pargs[] = {&pa};
+    NLSPN_HIP_TRY(hipLaunchKernel(pfn, dim3(elementwise_grid(N / (pvec ? 4 : 1))), dim3(256), pargs, 0, s));
+    if ((rc = check_launch("nlspn_propagate prologue"))) return rc;
+
+    // T fused iterations; list_pred[t] lands in pred_inter[t]
+    for (int t = 0; t < T; ++t) {
+        StepArgs a = r.a;
+        a.p_in = t == 0 ? workspace : static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
+        a.p_out = static_cast<char *>(pred_inter) + (size_t)t * N * es;
+        a.pred_out = t == T - 1 ? pred : nullptr;
+        if ((rc = launch(L, a, s))) return rc;
+    }
+    return NLSPN_OK;
+}
+
+struct nlspn_plan {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep, const void *conf,
+                      const void *aff_raw, int64_t aff_bstride, const void *off_raw, int64_t off_bstride,
+                      const float *gamma, void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out,
+                      void *workspace, int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags) {
+    if (!plan) return fail(NLSPN_EINVAL, "plan is null");
+    *plan = nullptr;
+    hipStream_t cs = nullptr;
+    NLSPN_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(cs);
+        return fail(NLSPN_EHIP, "hipStreamBeginCapture: %s", hipGetErrorString(e));
+    }
+    int rc = nlspn_propagate(dtype, pred_init, dep, conf, aff_raw, aff_bstride, off_raw, off_bstride, gamma,
+                             pred_inter, pred, aff_out, off_out, conf_out, workspace, B, H, W, kh, kw, T, kind,
+                             flags, cs);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(cs, &g);
+    (void)hipStreamDestroy(cs);
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess) return fail(NLSPN_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    hipGraphExec_t ge = nullptr;
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        return fail(NLSPN_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+    }
+    nlspn_plan *p = new nlspn_plan;
+    p->graph = g;
+    p->exec = ge;
+    *plan = p;
+    return NLSPN_OK;
+}
+
+int nlspn_plan_launch(nlspn_plan_t plan, void *stream) {
+    if (!plan) return fail(NLSPN_EINVAL, "plan is null");
+    NLSPN_HIP_TRY(hipGraphLaunch(plan->exec, as_stream(stream)));
+    return NLSPN_OK;
+}
+
+int nlspn_plan_destroy(nlspn_plan_t plan) {
+    if (!plan) return NLSPN_OK;
+    if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
+    if (plan->graph) (void)hipGraphDestroy(plan->graph);
+    delete plan;
+    return NLSPN_OK;
+}
+
+int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const void *bias, const void *offset,
+                       const void *mask, void *output, int B, int C, int H, int W, int Cout, int kh, int kw, int sh,
+                       int sw, int ph, int pw, int dh, int dw, int group, int deformable_group, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (!input || !weight || !offset || !mask || !output) return fail(NLSPN_EINVAL, "null required pointer");
+    if (B < 1 || C < 1 || H < 1 || W < 1 || Cout < 1 || kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 ||
+        group < 1 || deformable_group < 1 || ph < 0 || pw < 0)
+        return fail(NLSPN_EINVAL, "invalid DCN arguments");
+    if ((C % group) != 0 || (Cout % group) != 0)
+        return fail(NLSPN_EINVAL, "channels(%d) and channels_out(%d) must divide group(%d)", C, Cout, group);
+    if ((C % deformable_group) != 0)
+        return fail(NLSPN_EINVAL, "channels(%d) must divide deformable_group(%d)", C, deformable_group);
+    const int Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1;
+    const int Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
+    if (Ho < 1 || Wo < 1) return fail(NLSPN_EINVAL, "output size %dx%d is empty", Ho, Wo);
+    MdcnArgs a{input, weight, bias, offset, mask, output, B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+               group, deformable_group, Ho, Wo};
+    const void *fn = dtype == NLSPN_DTYPE_F32 ? reinterpret_cast<const void *>(&mdcn_forward_kernel<float>)
+                                              : reinterpret_cast<const void *>(&mdcn_forward_kernel<__half>);
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(elementwise_grid((long long)B * Cout * Ho * Wo)), dim3(256), args, 0,
+                                  as_stream(stream)));
+    return check_launch("nlspn_mdcn_forward");
+}
+
+int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const void *dep, const void *aff,
+                         int64_t aff_bstride, const void *off, int64_t off_bstride, int off_layout, void *p_out,
+                         int B, int H, int W, int kh, int kw, unsigned flags, int reps, void *stream, float *mean_ms,
+                         float *min_ms) {
+    if (reps < 1 || !mean_ms || !min_ms) return fail(NLSPN_EINVAL, "reps must be >= 1 and outputs non-null");
+    StepReq r{};
+    r.dtype = dtype;
+    r.kh = kh;
+    r.kw = kw;
+    r.a = StepArgs{p_in, conf, dep, aff, off, p_out, nullptr, aff_bstride, off_bstride, B, H, W, 0, 0,
+                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags};
+    StepLaunch L;
+    int rc = prepare_step(r, L);
+    if (rc) return rc;
+    hipStream_t s = as_stream(stream);
+    std::vector<hipEvent_t> ev(2 * (size_t)reps, nullptr);
+    for (auto &e : ev) NLSPN_HIP_TRY(hipEventCreate(&e));
+    for (int i = 0; i < reps && rc == 0; ++i) rc = launch(L, r.a, s, ev[2 * i], ev[2 * i + 1]);
+    hipError_t se = hipEventSynchronize(ev.back());
+    double sum = 0.0;
+    float mn = 1e30f;
+    if (rc == 0 && se == hipSuccess) {
+        for (int i = 0; i < reps; ++i) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) != hipSuccess) {
+                rc = fail(NLSPN_EHIP, "hipEventElapsedTime failed");
+                break;
+            }
+            sum += ms;
+            mn = ms < mn ? ms : mn;
+        }
+    } else if (rc == 0) {
+        rc = fail(NLSPN_EHIP, "hipEventSynchronize: %s", hipGetErrorString(se));
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    if (rc) return rc;
+    *mean_ms = (float)(sum / reps);
+    *min_ms = mn;
+    return NLSPN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// Shared device helpers for the NLSPN HIP kernels (gfx950 / CDNA4).
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nlspn {
+
+constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin (b, b+8 share one)
+
+// Element load/store with fp32 math regardless of storage type.
+template <typename T> __device__ __forceinline__ float ld(const T *p);
+template <> __device__ __forceinline__ float ld<float>(const float *p) { return *p; }
+template <> __device__ __forceinline__ float ld<__half>(const __half *p) { return __half2float(*p); }
+
+template <typename T> __device__ __forceinline__ void st(T *p, float v);
+template <> __device__ __forceinline__ void st<float>(float *p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st<__half>(__half *p, float v) { *p = __float2half(v); }
+
+// PX contiguous elements <-> float[PX]; PX>1 variants need PX*sizeof(T) alignment.
+template <typename T, int PX> struct Vec;
+
+template <> struct Vec<float, 1> {
+    static __device__ __forceinline__ void load(const float *p, float (&v)[1]) { v[0] = *p; }
+    static __device__ __forceinline__ void store(float *p, const float (&v)[1]) { *p = v[0]; }
+};
+template <> struct Vec<float, 4> {
+    static __device__ __forceinline__ void load(const float *p, float (&v)[4]) {
+        const float4 q = *reinterpret_cast<const float4 *>(p);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    }
+    static __device__ __forceinline__ void store(float *p, const float (&v)[4]) {
+        *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+template <> struct Vec<float, 2> {
+    static __device__ __forceinline__ void load(const float *p, float (&v)[2]) {
+        const float2 q = *reinterpret_cast<const float2 *>(p);
+        v[0] = q.x; v[1] = q.y;
+    }
+    static __device__ __forceinline__ void store(float *p, const float (&v)[2]) {
+        *reinterpret_cast<float2 *>(p) = make_float2(v[0], v[1]);
+    }
+};
+template <> struct Vec<__half, 2> {
+    static __device__ __forceinline__ void load(const __half *p, float (&v)[2]) {
+        const float2 f = __half22float2(*reinterpret_cast<const __half2 *>(p));
+        v[0] = f.x; v[1] = f.y;
+    }
+    static __device__ __forceinline__ void store(__half *p, const float (&v)[2]) {
+        *reinterpret_cast<__half2 *>(p) = __floats2half2_rn(v[0], v[1]);
+    }
+};
+template <> struct Vec<__half, 1> {
+    static __device__ __forceinline__ void load(const __half *p, float (&v)[1]) { v[0] = __half2float(*p); }
+    static __device__ __forceinline__ void store(__half *p, const float (&v)[1]) { *p = __float2half(v[0]); }
+};
+template <> struct Vec<__half, 4> {
+    static __device__ __forceinline__ void load(const __half *p, float (&v)[4]) {
+        const uint2 q = *reinterpret_cast<const uint2 *>(p);
+        const __half2 a = *reinterpret_cast<const __half2 *>(&q.x);
+        const __half2 b = *reinterpret_cast<const __half2 *>(&q.y);
+        const float2 fa = __half22float2(a), fb = __half22float2(b);
+        v[0] = fa.x; v[1] = fa.y; v[2] = fb.x; v[3] = fb.y;
+    }
+    static __device__ __forceinline__ void store(__half *p, const float (&v)[4]) {
+        uint2 q;
+        __half2 a = __floats2half2_rn(v[0], v[1]);
+        __half2 b = __floats2half2_rn(v[2], v[3]);
+        q.x = *reinterpret_cast<uint32_t *>(&a);
+        q.y = *reinterpret_cast<uint32_t *>(&b);
+        *reinterpret_cast<uint2 *>(p) = q;
+    }
+};
+
+// torch.clamp(x, min=0) (NaN propagates).
+__device__ __forceinline__ float clamp0(float v) { return v < 0.f ? 0.f : v; }
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5.5 T1): consecutive
+// logical tiles land on the same XCD so neighbouring tiles' halo reads of the
+// previous iteration's depth hit that XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+    const int q = nblk / kNumXcd, r = nblk % kNumXcd;
+    const int xcd = bid % kNumXcd, slot = bid / kNumXcd;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + slot;
+}
+
+}  // namespace nlspn

@@ -1,0 +1,93 @@
+"""Seam 2 of the drop-in: a `DCN`-compatible module backed by the HIP library.
+
+Reference: the pybind module `DCN` (src/model/deformconv/src/vision.cpp:6-13) whose
+`modulated_deform_conv_forward` NLSPN reaches through
+src/model/modulated_deform_conv_func.py:13,26 (ModulatedDeformConvFunction).
+Installing this module as `DCN` (``sys.modules['DCN'] = nlspn_eccv20_amd.dcn``)
+lets the unmodified reference nlspnmodel.py run its offset branch on MI355X.
+Only the forward is native this round; the backward (vision.cpp:10) is the next
+row of the build plan and raises.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+from torch.nn.modules.utils import _pair
+
+from . import _lib
+from .propagation import _cuda, _dtype_code, _ptr, _stream
+
+__all__ = ["modulated_deform_conv_forward", "modulated_deform_conv_backward", "ModulatedDeformConvFunction"]
+
+
+def modulated_deform_conv_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w,
+                                  pad_h, pad_w, dilation_h, dilation_w, group, deformable_group, im2col_step):
+    """Same signature and checks as modulated_deform_conv_cuda_forward
+    (modulated_deform_conv_cuda.cu:19-121); returns (B, Cout, Ho, Wo).  im2col_step is
+    accepted for signature compatibility; there is no columns buffer to chunk."""
+    if not input.is_contiguous():
+        raise RuntimeError("input tensor has to be contiguous")
+    if not weight.is_contiguous():
+        raise RuntimeError("weight tensor has to be contiguous")
+    for n, t in (("input", input), ("weight", weight), ("bias", bias), ("offset", offset), ("mask", mask)):
+        _cuda(n, t)
+    B, C, H, W = input.shape
+    Cout, Ckern, kh_, kw_ = weight.shape
+    if kh_ != kernel_h or kw_ != kernel_w:
+        raise RuntimeError(f"Input shape and kernel shape wont match: ({kernel_h} x {kernel_w} vs {kh_} x {kw_}).")
+    if C != Ckern * group:
+        raise RuntimeError(f"Input shape and kernel channels wont match: ({C} vs {Ckern * group}).")
+    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    KK = kernel_h * kernel_w
+    if tuple(offset.shape) != (B, 2 * deformable_group * KK, Ho, Wo):
+        raise RuntimeError(f"offset has shape {tuple(offset.shape)}, expected {(B, 2 * deformable_group * KK, Ho, Wo)}")
+    if tuple(mask.shape) != (B, deformable_group * KK, Ho, Wo):
+        raise RuntimeError(f"mask has shape {tuple(mask.shape)}, expected {(B, deformable_group * KK, Ho, Wo)}")
+    dt = input.dtype
+    offset, mask, weight = offset.contiguous(), mask.contiguous(), weight.contiguous()
+    if bias is not None:
+        bias = bias.contiguous()
+    for n, t in (("weight", weight), ("bias", bias), ("offset", offset), ("mask", mask)):
+        if t is not None and t.dtype != dt:
+            raise RuntimeError(f"{n} dtype {t.dtype} differs from input dtype {dt}")
+    out = torch.empty((B, Cout, Ho, Wo), dtype=dt, device=input.device)
+    with torch.cuda.device(input.device):
+        _lib.check(_lib.get().nlspn_mdcn_forward(
+            _dtype_code(input), _ptr(input), _ptr(weight), _ptr(bias), _ptr(offset), _ptr(mask), _ptr(out),
+            B, C, H, W, Cout, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+            group, deformable_group, _stream(input.device)))
+    return out
+
+
+def modulated_deform_conv_backward(*args, **kwargs):
+    """vision.cpp:10 — not native yet (build plan §8f rank 1)."""
+    raise NotImplementedError("modulated_deform_conv_backward is not implemented on MI355X yet")
+
+
+class ModulatedDeformConvFunction(Function):
+    """Mirror of src/model/modulated_deform_conv_func.py:15-56 (same apply() signature)."""
+
+    @staticmethod
+    def forward(ctx, input, offset, mask, weight, bias, stride, padding, dilation, groups, deformable_groups,
+                im2col_step):
+        ctx.stride = _pair(stride)
+        ctx.padding = _pair(padding)
+        ctx.dilation = _pair(dilation)
+        ctx.kernel_size = _pair(weight.shape[2:4])
+        ctx.groups = groups
+        ctx.deformable_groups = deformable_groups
+        ctx.im2col_step = im2col_step
+        output = modulated_deform_conv_forward(
+            input, weight, bias, offset, mask, ctx.kernel_size[0], ctx.kernel_size[1], ctx.stride[0], ctx.stride[1],
+            ctx.padding[0], ctx.padding[1], ctx.dilation[0], ctx.dilation[1], ctx.groups, ctx.deformable_groups,
+            ctx.im2col_step)
+        ctx.save_for_backward(input, offset, mask, weight, bias)
+        return output
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        return modulated_deform_conv_backward()
+

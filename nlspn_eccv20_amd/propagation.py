@@ -1,0 +1,318 @@
+"""MI355X-native NLSPN propagation — host-side mirror of the reference interface.
+
+Reference (XJTUXYC/NLSPN_ECCV20, src/model/nlspnmodel.py):
+  _affinity_normalization :179-201   -> affinity_normalization()
+  _aff_insert             :261-269   -> (fused into affinity_normalization)
+  _off_insert             :252-259   -> off_insert()
+  _propagate_once         :203-226   -> prop_step() (fused with :351 and :355-361)
+  forward, propagation    :317-383   -> propagate() / NLSPNPropagation.forward()
+
+Every call goes through the C ABI in include/nlspn_prop.h (HIP kernels for
+gfx950); there is no CPU path.  Tensors are NCHW with contiguous (H, W) planes;
+per-batch strides are passed through, so the (B, 3K, H, W) head output can be
+sliced into offsets/affinities without a copy (nlspnmodel.py:304-305).
+Computation is fp32; storage may be fp32 or fp16.
+
+These functional ops are inference ops (not differentiable); the backward of
+the fused step is the next row of the build plan.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+__all__ = [
+    "affinity_normalization", "off_insert", "prop_step", "propagate", "PropagationPlan",
+    "NLSPNPropagation", "kernel_geometry",
+]
+
+
+# ----------------------------------------------------------------- helpers
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return _lib.DTYPE_F32
+    if t.dtype == torch.float16:
+        return _lib.DTYPE_F16
+    raise TypeError(f"NLSPN propagation supports float32 and float16 storage, got {t.dtype}")
+
+
+def _cuda(name: str, t: Optional[torch.Tensor]) -> None:
+    # modulated_deform_conv_cuda.cu:42-46 ("... must be a CUDA tensor")
+    if t is not None and not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _planes(name: str, t: torch.Tensor, B: int, C: Optional[int], H: int, W: int) -> int:
+    """Check (B, C, H, W) with contiguous H*W planes, consecutive within a batch item;
+    return the batch stride in elements."""
+    if t.dim() != 4 or t.shape[0] != B or tuple(t.shape[2:]) != (H, W) or (C is not None and t.shape[1] != C):
+        want = f"({B}, {C if C is not None else '*'}, {H}, {W})"
+        raise RuntimeError(f"{name} has shape {tuple(t.shape)}, expected {want}")
+    if t.stride(3) != 1 or (H > 1 and t.stride(2) != W) or (t.shape[1] > 1 and t.stride(1) != H * W):
+        raise RuntimeError(f"{name} tensor has to have contiguous H*W planes")
+    return t.stride(0) if B > 1 else t.shape[1] * H * W
+
+
+def kernel_geometry(prop_kernel) -> Tuple[int, int]:
+    """prop_kernel int k -> (k, k); or an explicit (kh, kw).  Odd sizes only
+    (nlspnmodel.py:29-30).  K = kh*kw - 1 neighbours."""
+    kh, kw = (prop_kernel, prop_kernel) if isinstance(prop_kernel, int) else tuple(prop_kernel)
+    if kh % 2 != 1 or kw % 2 != 1:
+        raise AssertionError(f"only odd kernel is supported but k_f = {prop_kernel}")
+    return int(kh), int(kw)
+
+
+def _gamma_f32(gamma) -> torch.Tensor:
+    if not torch.is_tensor(gamma):
+        raise TypeError("gamma must be a device tensor (aff_scale_const)")
+    g = gamma.detach().reshape(-1)[:1]
+    return g if g.dtype == torch.float32 else g.float()
+
+
+def _no_grad_inputs(*ts) -> None:
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
+        raise NotImplementedError(
+            "the fused NLSPN propagation has no backward yet (build plan §8f rank 1); "
+            "call it under torch.no_grad() / in eval mode")
+
+
+# -------------------------------------------------------------- functional ops
+def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "TGASS") -> torch.Tensor:
+    """NLSPNModel._affinity_normalization + _aff_insert (nlspnmodel.py:179-201, :261-269).
+    aff (B, K, H, W) raw -> (B, K+1, H, W), reference tap at K//2."""
+    _cuda("aff", aff)
+    if kind not in _lib.AFF_KINDS:
+        raise NotImplementedError(kind)
+    B, K, H, W = aff.shape
+    bs = _planes("aff", aff, B, K, H, W)
+    g = _gamma_f32(gamma)
+    out = torch.empty((B, K + 1, H, W), dtype=aff.dtype, device=aff.device)
+    with torch.cuda.device(aff.device):
+        _lib.check(_lib.get().nlspn_affinity_normalize(
+            _dtype_code(aff), _ptr(aff), bs, _ptr(g), _ptr(out), B, K, H, W, _lib.AFF_KINDS[kind],
+            _stream(aff.device)))
+    return out
+
+
+def off_insert(offset: torch.Tensor) -> torch.Tensor:
+    """NLSPNModel._off_insert (nlspnmodel.py:252-259): (B, 2K, H, W) -> (B, 2(K+1), H, W)
+    with a zero (dh, dw) pair at tap K//2.  A layout conversion, kept in torch."""
+    B, K2, H, W = offset.shape
+    K = K2 // 2
+    o = offset.reshape(B, K, 2, H, W)
+    z = torch.zeros((B, 1, 2, H, W), dtype=offset.dtype, device=offset.device)
+    return torch.cat([o[:, :K // 2], z, o[:, K // 2:]], 1).reshape(B, -1, H, W)
+
+
+def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optional[torch.Tensor],
+              aff: torch.Tensor, offset: Optional[torch.Tensor] = None, *, kernel=(3, 3),
+              offset_layout: str = "inserted", preserve_input: bool = True, always_clip: bool = False,
+              out: Optional[torch.Tensor] = None, pred_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One fused iteration (nlspnmodel.py:350-361): out = _propagate_once(feat*confidence,
+    offset, aff), then the preserve-input blend with dep and the optional clamp.
+
+    aff: normalised (B, K+1, H, W) (the output of affinity_normalization; its tap K//2 is
+    recomputed in-kernel as 1 - sum of the others).  offset: (B, 2(K+1), H, W) inserted
+    layout or (B, 2K, H, W) with offset_layout="raw"; None = no-offset branch (3x3 replicate).
+    """
+    kh, kw = kernel_geometry(kernel)
+    K = kh * kw - 1
+    for n, t in (("feat", feat), ("confidence", confidence), ("dep", dep), ("aff", aff), ("offset", offset)):
+        _cuda(n, t)
+    B, _, H, W = feat.shape
+    _planes("feat", feat, B, 1, H, W)
+    if not feat.is_contiguous():
+        raise RuntimeError("input tensor has to be contiguous")
+    for n, t in (("confidence", confidence), ("dep", dep)):
+        if t is not None:
+            _planes(n, t, B, 1, H, W)
+            if t.dtype != feat.dtype or not t.is_contiguous():
+                raise RuntimeError(f"{n} must be contiguous with feat's dtype")
+    if preserve_input and dep is None:
+        raise RuntimeError("preserve_input requires dep")
+    abs_ = _planes("aff", aff, B, K + 1, H, W)
+    layout = _lib.OFF_RAW if offset_layout == "raw" else _lib.OFF_INSERTED
+    obs = 0
+    if offset is not None:
+        obs = _planes("offset", offset, B, 2 * K if layout == _lib.OFF_RAW else 2 * (K + 1), H, W)
+    if out is None:
+        out = torch.empty_like(feat)
+    flags = (_lib.PRESERVE_INPUT if preserve_input else 0) | (_lib.ALWAYS_CLIP if always_clip else 0)
+    with torch.cuda.device(feat.device):
+        _lib.check(_lib.get().nlspn_prop_step(
+            _dtype_code(feat), _ptr(feat), _ptr(confidence), _ptr(dep), _ptr(aff), abs_, _ptr(offset), obs,
+            layout, _ptr(out), _ptr(pred_out), B, H, W, kh, kw, flags, _stream(feat.device)))
+    return out
+
+
+def _alloc_outputs(pred_init, K, T, with_off, with_conf):
+    B, _, H, W = pred_init.shape
+    kw_ = dict(dtype=pred_init.dtype, device=pred_init.device)
+    return {
+        "pred_inter": torch.empty((T, B, 1, H, W), **kw_),
+        "pred": torch.empty((B, 1, H, W), **kw_),
+        "aff": torch.empty((B, K + 1, H, W), **kw_),
+        "offset": torch.empty((B, 2 * (K + 1), H, W), **kw_) if with_off else None,
+        "confidence": torch.empty((B, 1, H, W), **kw_) if with_conf else None,
+        "workspace": torch.empty((B, 1, H, W), **kw_),
+    }
+
+
+def _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
+                    preserve_input, always_clip, outs):
+    kh, kw = kernel_geometry(kernel)
+    K = kh * kw - 1
+    for n, t in (("pred_init", pred_init), ("dep", dep), ("confidence", confidence), ("aff", aff),
+                 ("offset", offset), ("gamma", gamma)):
+        _cuda(n, t)
+    if affinity not in _lib.AFF_KINDS:
+        raise NotImplementedError(affinity)
+    B, C, H, W = pred_init.shape
+    if C != 1:
+        raise AssertionError("ch_f must equal pred_init.shape[1] == 1 (nlspnmodel.py:318)")
+    _planes("pred_init", pred_init, B, 1, H, W)
+    dt = pred_init.dtype
+    for n, t in (("dep", dep), ("confidence", confidence)):
+        if t is not None:
+            _planes(n, t, B, 1, H, W)
+            if not t.is_contiguous() or t.dtype != dt:
+                raise RuntimeError(f"{n} must be contiguous with pred_init's dtype")
+    if not pred_init.is_contiguous():
+        raise RuntimeError("pred_init must be contiguous")
+    if preserve_input and dep is None:
+        raise RuntimeError("preserve_input requires dep")
+    abs_ = _planes("aff", aff, B, K, H, W)
+    obs = _planes("offset", offset, B, 2 * K, H, W) if offset is not None else 0
+    if aff.dtype != dt or (offset is not None and offset.dtype != dt):
+        raise RuntimeError("aff/offset must have pred_init's dtype")
+    flags = (_lib.PRESERVE_INPUT if preserve_input else 0) | (_lib.ALWAYS_CLIP if always_clip else 0)
+    g = _gamma_f32(gamma)
+    args = (_dtype_code(pred_init), _ptr(pred_init), _ptr(dep), _ptr(confidence), _ptr(aff), abs_,
+            _ptr(offset), obs, _ptr(g), _ptr(outs["pred_inter"]), _ptr(outs["pred"]), _ptr(outs["aff"]),
+            _ptr(outs["offset"]), _ptr(outs["confidence"]), _ptr(outs["workspace"]),
+            B, H, W, kh, kw, int(prop_time), _lib.AFF_KINDS[affinity], flags)
+    return args, g
+
+
+def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: Optional[torch.Tensor],
+              aff: torch.Tensor, offset: Optional[torch.Tensor], gamma: torch.Tensor, *, prop_time: int = 18,
+              affinity: str = "TGASS", kernel=(3, 3), preserve_input: bool = True, always_clip: bool = False,
+              return_offset: bool = True) -> dict:
+    """The propagation section of NLSPNModel.forward (nlspnmodel.py:323-381), fused:
+    1 prologue launch + prop_time iteration launches on the current stream.
+
+    aff: raw affinity (B, K, H, W); offset: raw offsets (B, 2K, H, W) or None;
+    gamma: aff_scale_const (device tensor, read on the device).
+    Returns {'pred', 'pred_inter' (list of prop_time (B,1,H,W) views), 'offset'
+    (inserted, or None), 'aff' (normalised, K+1 taps), 'confidence' (blended, or None)}.
+    """
+    kh, kw = kernel_geometry(kernel)
+    outs = _alloc_outputs(pred_init, kh * kw - 1, prop_time, offset is not None and return_offset,
+                          confidence is not None)
+    args, _ = _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
+                              preserve_input, always_clip, outs)
+    with torch.cuda.device(pred_init.device):
+        _lib.check(_lib.get().nlspn_propagate(*args, _stream(pred_init.device)))
+    return {"pred": outs["pred"], "pred_inter": list(outs["pred_inter"].unbind(0)), "offset": outs["offset"],
+            "aff": outs["aff"], "confidence": outs["confidence"], "pred_inter_tensor": outs["pred_inter"]}
+
+
+class PropagationPlan:
+    """propagate() captured once into a native hipGraph (nlspn_plan_create) over fixed
+    input/output buffers; replay() re-runs the whole section with one hipGraphLaunch.
+    Refill the input tensors in place between replays; γ is read on the device."""
+
+    def __init__(self, pred_init, dep, confidence, aff, offset, gamma, *, prop_time=18, affinity="TGASS",
+                 kernel=(3, 3), preserve_input=True, always_clip=False, return_offset=True):
+        kh, kw = kernel_geometry(kernel)
+        self.device = pred_init.device
+        self.outputs = _alloc_outputs(pred_init, kh * kw - 1, prop_time, offset is not None and return_offset,
+                                      confidence is not None)
+        args, g = _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
+                                  preserve_input, always_clip, self.outputs)
+        self._keep = (pred_init, dep, confidence, aff, offset, g)  # buffers baked into the graph
+        self._plan = ctypes.c_void_p()
+        self._lib = _lib.get()
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.nlspn_plan_create(ctypes.byref(self._plan), *args))
+
+    def replay(self) -> dict:
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.nlspn_plan_launch(self._plan, _stream(self.device)))
+        o = self.outputs
+        return {"pred": o["pred"], "pred_inter": list(o["pred_inter"].unbind(0)), "offset": o["offset"],
+                "aff": o["aff"], "confidence": o["confidence"], "pred_inter_tensor": o["pred_inter"]}
+
+    def close(self) -> None:
+        if getattr(self, "_plan", None) is not None and self._plan.value:
+            self._lib.nlspn_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# -------------------------------------------------------------- nn.Module
+class NLSPNPropagation(nn.Module):
+    """The propagation state and section of NLSPNModel (nlspnmodel.py:88-121, :317-383)
+    as a module.  Reads the reference's args attribute names: prop_kernel (int, or an
+    (kh, kw) tuple via args.prop_kernel_hw), affinity, affinity_gamma, prop_time,
+    preserve_input, always_clip, conf_prop, offset.  Parameters keep the reference's
+    state_dict names and shapes: aff_scale_const, w, b, w_conf."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.args = args
+        kernel = getattr(args, "prop_kernel_hw", None) or args.prop_kernel
+        self.kh, self.kw = kernel_geometry(kernel)
+        self.num_neighbors = self.kh * self.kw - 1
+        self.ch_f = 1
+        self.idx_ref = self.num_neighbors // 2
+        if args.affinity == "TC":
+            self.aff_scale_const = nn.Parameter(self.num_neighbors * torch.ones(1), requires_grad=False)
+        elif args.affinity == "TGASS":
+            self.aff_scale_const = nn.Parameter(args.affinity_gamma * self.num_neighbors * torch.ones(1))
+        elif args.affinity in ("AS", "ASS"):
+            self.aff_scale_const = nn.Parameter(torch.ones(1), requires_grad=False)
+        else:
+            raise NotImplementedError
+        # dummy gathering parameters, kept so reference checkpoints load (nlspnmodel.py:107-114)
+        self.w = nn.Parameter(torch.ones((self.ch_f, 1, self.kh, self.kw)), requires_grad=False)
+        self.b = nn.Parameter(torch.zeros(self.ch_f), requires_grad=False)
+        self.w_conf = nn.Parameter(torch.ones((1, 1, 1, 1)), requires_grad=False)
+
+    def forward(self, pred_init, dep, off_aff, confidence=None) -> dict:
+        a = self.args
+        K = self.num_neighbors
+        if a.offset:
+            off, aff = off_aff[:, :2 * K], off_aff[:, 2 * K:]   # nlspnmodel.py:303-305
+        else:
+            off, aff = None, off_aff
+        if not a.conf_prop:
+            confidence = None
+        if self.training:
+            _no_grad_inputs(pred_init, dep, off_aff, confidence, self.aff_scale_const)
+        with torch.no_grad():
+            out = propagate(pred_init.detach(), dep, None if confidence is None else confidence.detach(),
+                            aff.detach(), None if off is None else off.detach(), self.aff_scale_const,
+                            prop_time=a.prop_time, affinity=a.affinity, kernel=(self.kh, self.kw),
+                            preserve_input=a.preserve_input, always_clip=a.always_clip)
+        return {"pred": out["pred"], "pred_init": pred_init, "pred_inter": out["pred_inter"],
+                "offset": out["offset"], "aff": out["aff"], "gamma": self.aff_scale_const.data,
+                "confidence": out["confidence"]}

@@ -1,0 +1,238 @@
+/*
+ * ORACLE BODY — test infrastructure only; never linked into the product path.
+ *
+ * Precision-generic body of the CPU restatement of NLSPN's propagation section.
+ * Included twice by nlspn_oracle.c, once with REAL=float (suffix _f32) and once
+ * with REAL=double (suffix _f64).  Every function cites the reference lines it
+ * restates (paths relative to the reference repo root).
+ *
+ * Arithmetic is written in the reference's own operation order so that, built
+ * with -ffp-contract=off, the float instance is the exact IEEE sequence the
+ * reference issues (modulo the order ATen/BLAS picks for its sums, which the
+ * reference does not pin; sums here run over the tap/channel index in order).
+ */
+
+/* nlspnmodel.py:179-201 (_affinity_normalization) + :261-269 (_aff_insert).
+ * aff_raw: B x K planes of HW, batch stride aff_bstride (elements).
+ * aff_out: B x (K+1) planes of HW, contiguous; reference tap at K/2. */
+void FN(orc_aff_norm)(const REAL *aff_raw, long long aff_bstride, int B, int K,
+                      long long HW, int kind, REAL gamma, REAL *aff_out)
+{
+    const int ref = K / 2;                        /* nlspnmodel.py:91 idx_ref */
+    const long long ob = (long long)(K + 1) * HW;
+#pragma omp parallel for num_threads(orc_threads) schedule(static)
+    for (long long bp = 0; bp < (long long)B * HW; ++bp) {
+        const long long b = bp / HW, p = bp % HW;
+        REAL t[64];
+        REAL s = 0;
+        for (int k = 0; k < K; ++k) {
+            REAL a = aff_raw[b * aff_bstride + k * HW + p];
+            if (kind == ORC_TC)                   /* :182-183 tanh(aff)/gamma */
+                a = TANH(a) / gamma;
+            else if (kind == ORC_TGASS)           /* :184-185 tanh(aff)/(gamma+1e-8) */
+                a = TANH(a) / (gamma + (REAL)1e-8);
+            t[k] = a;
+        }
+        for (int k = 0; k < K; ++k)               /* :190-191 sum |aff| (+1e-4 below) */
+            s += FABS(t[k]);
+        s = s + (REAL)1e-4;
+        if (kind == ORC_ASS || kind == ORC_TGASS) /* :193-194 clamp sum to >= 1 */
+            if (s < (REAL)1.0) s = (REAL)1.0;
+        if (kind != ORC_TC)                       /* :196-197 divide (AS/ASS/TGASS) */
+            for (int k = 0; k < K; ++k) t[k] = t[k] / s;
+        REAL sum = 0;                             /* :262-263 aff_ref = 1 - sum(aff) */
+        for (int k = 0; k < K; ++k) sum += t[k];
+        REAL aref = (REAL)1.0 - sum;
+        REAL *o = aff_out + b * ob + p;
+        for (int k = 0, c = 0; c < K + 1; ++c) {  /* :265-267 insert at idx_ref */
+            if (c == ref) o[c * HW] = aref;
+            else o[c * HW] = t[k++];
+        }
+    }
+}
+
+/* nlspnmodel.py:252-259 (_off_insert): view (B,K,2,H,W), insert a zero (dh,dw)
+ * pair at tap idx_ref -> (B, 2(K+1), H, W). */
+void FN(orc_off_insert)(const REAL *off_raw, long long off_bstride, int B, int K,
+                        long long HW, REAL *off_out)
+{
+    const int ref = K / 2;
+    for (int b = 0; b < B; ++b)
+        for (int c = 0, k = 0; c < K + 1; ++c) {
+            REAL *o = off_out + ((long long)b * 2 * (K + 1) + 2 * c) * HW;
+            if (c == ref) {
+                for (long long p = 0; p < 2 * HW; ++p) o[p] = 0;
+            } else {
+                const REAL *s = off_raw + b * off_bstride + 2LL * k * HW;
+                for (long long p = 0; p < 2 * HW; ++p) o[p] = s[p];
+                ++k;
+            }
+        }
+}
+
+/* modulated_deform_im2col_cuda.cuh:24-54 (mdmcn_im2col_bilinear), zero
+ * contribution from out-of-image corners. */
+static REAL FN(orc_bilinear)(const REAL *im, int H, int W, REAL h, REAL w)
+{
+    int h_low = (int)FLOOR(h);
+    int w_low = (int)FLOOR(w);
+    int h_high = h_low + 1;
+    int w_high = w_low + 1;
+    REAL lh = h - h_low;
+    REAL lw = w - w_low;
+    REAL hh = 1 - lh, hw = 1 - lw;
+    REAL v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+    if (h_low >= 0 && w_low >= 0) v1 = im[(long long)h_low * W + w_low];
+    if (h_low >= 0 && w_high <= W - 1) v2 = im[(long long)h_low * W + w_high];
+    if (h_high <= H - 1 && w_low >= 0) v3 = im[(long long)h_high * W + w_low];
+    if (h_high <= H - 1 && w_high <= W - 1) v4 = im[(long long)h_high * W + w_high];
+    REAL w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+    return (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
+}
+
+/* Modulated DCNv2 forward specialised to NLSPN's use: channels = out channels = 1,
+ * stride 1, dilation 1, deformable_group 1, weight all ones, bias zero
+ * (nlspnmodel.py:107-121, :205-207).
+ *   modulated_deform_im2col_cuda.cuh:127-194: per tap (i,j) in row-major order,
+ *     h_im = (y - pad_h + i) + dh, w_im = (x - pad_w + j) + dw, sampled only if
+ *     h_im > -1 && w_im > -1 && h_im < H && w_im < W, col = val * mask;
+ *   modulated_deform_conv_cuda.cu:108-114: out = bias + sum_t col_t * weight_t.
+ * off: B x 2*kh*kw planes (dh plane 2t, dw plane 2t+1); mask: B x kh*kw planes. */
+void FN(orc_mdcn_c1)(const REAL *im, const REAL *off, const REAL *mask,
+                     int B, int H, int W, int kh, int kw, int ph, int pw, REAL *out)
+{
+    const long long HW = (long long)H * W;
+    const int KK = kh * kw;
+#pragma omp parallel for collapse(2) num_threads(orc_threads) schedule(static)
+    for (int b = 0; b < B; ++b)
+        for (int y = 0; y < H; ++y) {
+            const REAL *imb = im + b * HW;
+            const REAL *offb = off + (long long)b * 2 * KK * HW;
+            const REAL *mb = mask + (long long)b * KK * HW;
+            for (int x = 0; x < W; ++x) {
+                const long long p = (long long)y * W + x;
+                REAL acc = 0;
+                for (int i = 0; i < kh; ++i)
+                    for (int j = 0; j < kw; ++j) {
+                        const int t = i * kw + j;
+                        const REAL dh = offb[(2LL * t) * HW + p];
+                        const REAL dw = offb[(2LL * t + 1) * HW + p];
+                        const REAL m = mb[(long long)t * HW + p];
+                        REAL val = 0;
+                        const REAL h_im = (y - ph + i) + dh;
+                        const REAL w_im = (x - pw + j) + dw;
+                        if (h_im > -1 && w_im > -1 && h_im < H && w_im < W)
+                            val = FN(orc_bilinear)(imb, H, W, h_im, w_im);
+                        acc += val * m;
+                    }
+                out[b * HW + p] = acc;
+            }
+        }
+}
+
+/* nlspnmodel.py:209-224: no-offset branch. Replicate pad by 1, the 9 shifted
+ * slices in row-major (dy,dx) order, times aff (B,9,H,W), summed over taps.
+ * The reference hard-codes 3x3 here regardless of prop_kernel. */
+void FN(orc_prop_noffset)(const REAL *feat, const REAL *aff, int B, int H, int W, REAL *out)
+{
+    const long long HW = (long long)H * W;
+#pragma omp parallel for collapse(2) num_threads(orc_threads) schedule(static)
+    for (int b = 0; b < B; ++b)
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                const REAL *fb = feat + b * HW;
+                const REAL *ab = aff + (long long)b * 9 * HW;
+                REAL acc = 0;
+                for (int t = 0; t < 9; ++t) {
+                    int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+                    yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+                    xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+                    acc += fb[(long long)yy * W + xx] * ab[(long long)t * HW + (long long)y * W + x];
+                }
+                out[b * HW + (long long)y * W + x] = acc;
+            }
+}
+
+static REAL FN(orc_clamp0)(REAL v) { return v < 0 ? (REAL)0 : v; }  /* torch.clamp(min=0) */
+
+/* The whole propagation section, nlspnmodel.py:323-381:
+ *   :323-325 off = _off_insert(off); aff = _affinity_normalization(aff)
+ *   :328-334 mask_fix = (dep > 0); conf = (1-m)*conf + m
+ *   :340-363 T iterations of  p = propagate_once(p*conf, off, aff);
+ *            p = (1-m)*p + m*dep;  clamp if always_clip;  list_pred.append(p)
+ *            (k == 1 first applies the blend/clamp to pred_init, :341-348)
+ *   :375-377 pred = clamp(p, 0) unless always_clip.
+ * off_raw == NULL selects the no-offset branch (3x3 replicate, K must be 8).
+ * Returns 0 on success, nonzero on invalid arguments. */
+int FN(orc_propagate)(const REAL *pred_init, const REAL *dep, const REAL *conf,
+                      const REAL *aff_raw, long long aff_bstride,
+                      const REAL *off_raw, long long off_bstride,
+                      REAL gamma, int kind, int kh, int kw, int T, unsigned flags,
+                      int B, int H, int W,
+                      REAL *pred_inter, REAL *pred, REAL *aff_out, REAL *off_out, REAL *conf_out)
+{
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    const int K = kh * kw - 1;
+    const int preserve = (flags & ORC_PRESERVE) != 0;
+    const int clip = (flags & ORC_ALWAYS_CLIP) != 0;
+    if (K < 1 || K > 63 || (kh % 2) == 0 || (kw % 2) == 0 || T < 1) return 1;
+    if (off_raw == NULL && K != 8) return 2;
+    if (preserve && dep == NULL) return 3;
+
+    REAL *off_ins = NULL;
+    if (off_raw) {
+        off_ins = off_out ? off_out : (REAL *)malloc(sizeof(REAL) * 2 * (K + 1) * N);
+        FN(orc_off_insert)(off_raw, off_bstride, B, K, HW, off_ins);
+    }
+    FN(orc_aff_norm)(aff_raw, aff_bstride, B, K, HW, kind, gamma, aff_out);
+
+    REAL *cf = NULL;
+    if (conf) {
+        cf = conf_out ? conf_out : (REAL *)malloc(sizeof(REAL) * N);
+        for (long long i = 0; i < N; ++i) {
+            REAL c = conf[i];
+            if (preserve) {
+                REAL m = dep[i] > 0 ? (REAL)1 : (REAL)0;
+                c = ((REAL)1.0 - m) * c + m;
+            }
+            cf[i] = c;
+        }
+    }
+
+    REAL *p = (REAL *)malloc(sizeof(REAL) * N);
+    REAL *f = (REAL *)malloc(sizeof(REAL) * N);
+    for (long long i = 0; i < N; ++i) {
+        REAL v = pred_init[i];
+        if (preserve) {
+            REAL m = dep[i] > 0 ? (REAL)1 : (REAL)0;
+            v = ((REAL)1.0 - m) * v + m * dep[i];
+        }
+        if (clip) v = FN(orc_clamp0)(v);
+        p[i] = v;
+    }
+    for (int k = 0; k < T; ++k) {
+        for (long long i = 0; i < N; ++i) f[i] = cf ? p[i] * cf[i] : p[i];
+        if (off_ins)
+            FN(orc_mdcn_c1)(f, off_ins, aff_out, B, H, W, kh, kw, (kh - 1) / 2, (kw - 1) / 2, p);
+        else
+            FN(orc_prop_noffset)(f, aff_out, B, H, W, p);
+        REAL *o = pred_inter + (long long)k * N;
+        for (long long i = 0; i < N; ++i) {
+            REAL v = p[i];
+            if (preserve) {
+                REAL m = dep[i] > 0 ? (REAL)1 : (REAL)0;
+                v = ((REAL)1.0 - m) * v + m * dep[i];
+            }
+            if (clip) v = FN(orc_clamp0)(v);
+            p[i] = v;
+            o[i] = v;
+        }
+    }
+    for (long long i = 0; i < N; ++i) pred[i] = clip ? p[i] : FN(orc_clamp0)(p[i]);
+
+    free(p);
+    free(f);
+    if (off_ins && off_ins != off_out) free(off_ins);
+    if (cf && cf != conf_out) free(cf);
+    return 0;
+}

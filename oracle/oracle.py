@@ -1,0 +1,148 @@
+"""ORACLE (test infrastructure only) — numpy/ctypes front end of the C restatement.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this module.  It loads ``oracle/build/liborc_nlspn.so`` (built by
+``oracle/Makefile``), a plain-C restatement of the reference propagation section
+(``src/model/nlspnmodel.py:179-381`` and the DCNv2 forward
+``src/model/deformconv/src/cuda/modulated_deform_im2col_cuda.cuh:24-54,127-194``).
+It is the checker, never the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborc_nlspn.so")
+
+AFFINITY_KINDS = {"AS": 0, "ASS": 1, "TC": 2, "TGASS": 3}
+PRESERVE = 1
+ALWAYS_CLIP = 2
+
+_lib = None
+
+
+def build() -> str:
+    """Compile the oracle with gcc (make)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        for sfx in ("f32", "f64"):
+            getattr(_lib, f"orc_propagate_{sfx}").restype = ctypes.c_int
+        _lib.orc_get_threads.restype = ctypes.c_int
+    return _lib
+
+
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(int(n))
+
+
+def _sfx(dtype):
+    dtype = np.dtype(dtype)
+    if dtype == np.float32:
+        return "f32", ctypes.c_float
+    if dtype == np.float64:
+        return "f64", ctypes.c_double
+    raise TypeError(f"oracle supports float32/float64, got {dtype}")
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+def affinity_normalization(aff_raw, kind="TGASS", gamma=4.0):
+    """nlspnmodel.py:179-201 + :261-269 on a (B,K,H,W) array -> (B,K+1,H,W)."""
+    dtype = aff_raw.dtype
+    sfx, cr = _sfx(dtype)
+    a = _c(aff_raw, dtype)
+    B, K, H, W = a.shape
+    out = np.empty((B, K + 1, H, W), dtype=dtype)
+    getattr(lib(), f"orc_aff_norm_{sfx}")(
+        _p(a), ctypes.c_longlong(K * H * W), B, K, ctypes.c_longlong(H * W),
+        AFFINITY_KINDS[kind], cr(gamma), _p(out))
+    return out
+
+
+def off_insert(off_raw):
+    """nlspnmodel.py:252-259 on a (B,2K,H,W) array -> (B,2(K+1),H,W)."""
+    dtype = off_raw.dtype
+    sfx, _ = _sfx(dtype)
+    o = _c(off_raw, dtype)
+    B, K2, H, W = o.shape
+    K = K2 // 2
+    out = np.empty((B, 2 * (K + 1), H, W), dtype=dtype)
+    getattr(lib(), f"orc_off_insert_{sfx}")(
+        _p(o), ctypes.c_longlong(K2 * H * W), B, K, ctypes.c_longlong(H * W), _p(out))
+    return out
+
+
+def mdcn_c1(im, off, mask, kh=3, kw=3, ph=None, pw=None):
+    """DCNv2 forward for NLSPN's use (C=1, weight 1, bias 0); .cuh:127-194 + .cu:108-114."""
+    dtype = im.dtype
+    sfx, _ = _sfx(dtype)
+    im, off, mask = (_c(x, dtype) for x in (im, off, mask))
+    B, _, H, W = im.shape
+    ph = (kh - 1) // 2 if ph is None else ph
+    pw = (kw - 1) // 2 if pw is None else pw
+    out = np.empty((B, 1, H, W), dtype=dtype)
+    getattr(lib(), f"orc_mdcn_c1_{sfx}")(_p(im), _p(off), _p(mask), B, H, W, kh, kw, ph, pw, _p(out))
+    return out
+
+
+def prop_noffset(feat, aff):
+    """nlspnmodel.py:209-224 (replicate-pad 3x3 gather)."""
+    dtype = feat.dtype
+    sfx, _ = _sfx(dtype)
+    feat, aff = _c(feat, dtype), _c(aff, dtype)
+    B, _, H, W = feat.shape
+    out = np.empty((B, 1, H, W), dtype=dtype)
+    getattr(lib(), f"orc_prop_noffset_{sfx}")(_p(feat), _p(aff), B, H, W, _p(out))
+    return out
+
+
+def propagate(pred_init, dep, conf, aff_raw, off_raw, gamma, *, kind="TGASS", kh=3, kw=3,
+              prop_time=18, preserve_input=True, always_clip=False):
+    """Whole propagation section, nlspnmodel.py:323-381.
+
+    aff_raw (B,K,H,W) and off_raw (B,2K,H,W) or None (no-offset branch).
+    Returns dict with pred, pred_inter (T,B,1,H,W), aff (B,K+1,H,W),
+    offset (B,2(K+1),H,W) or None, confidence (B,1,H,W) or None.
+    """
+    dtype = pred_init.dtype
+    sfx, cr = _sfx(dtype)
+    pred_init, dep, conf, aff_raw, off_raw = (_c(x, dtype) for x in (pred_init, dep, conf, aff_raw, off_raw))
+    B, _, H, W = pred_init.shape
+    K = kh * kw - 1
+    assert aff_raw.shape == (B, K, H, W), aff_raw.shape
+    if off_raw is not None:
+        assert off_raw.shape == (B, 2 * K, H, W), off_raw.shape
+    flags = (PRESERVE if preserve_input else 0) | (ALWAYS_CLIP if always_clip else 0)
+    pred_inter = np.empty((prop_time, B, 1, H, W), dtype=dtype)
+    pred = np.empty((B, 1, H, W), dtype=dtype)
+    aff_out = np.empty((B, K + 1, H, W), dtype=dtype)
+    off_out = None if off_raw is None else np.empty((B, 2 * (K + 1), H, W), dtype=dtype)
+    conf_out = None if conf is None else np.empty((B, 1, H, W), dtype=dtype)
+    rc = getattr(lib(), f"orc_propagate_{sfx}")(
+        _p(pred_init), _p(dep), _p(conf),
+        _p(aff_raw), ctypes.c_longlong(K * H * W),
+        _p(off_raw), ctypes.c_longlong(2 * K * H * W),
+        cr(gamma), AFFINITY_KINDS[kind], kh, kw, prop_time, flags, B, H, W,
+        _p(pred_inter), _p(pred), _p(aff_out), _p(off_out), _p(conf_out))
+    if rc != 0:
+        raise ValueError(f"oracle propagate rejected its arguments (code {rc})")
+    return {"pred": pred, "pred_inter": pred_inter, "aff": aff_out,
+            "offset": off_out, "confidence": conf_out}

@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the REFERENCE's own Python (runs only in the build
+container, where /root/reference is mounted; never on the GPU box).
+
+What runs is the reference code itself (XJTUXYC/NLSPN_ECCV20, src/model/nlspnmodel.py):
+  * NLSPNModel._affinity_normalization  (:179-201) + _aff_insert (:261-269)
+  * NLSPNModel._off_insert              (:252-259)
+  * NLSPNModel._propagate_once, no-offset branch (:209-224)
+  * NLSPNModel.forward propagation section (:317-383), with the CNN encoder/decoder
+    heads replaced by callables that return fixed synthetic tensors (pred_init,
+    off_aff, confidence) so the loop runs on chosen inputs.
+
+Import needs two empty sys.modules entries: `torchvision` (only used to build the
+ResNet encoder, src/model/common.py:18,27-42, never called here) and `DCN` (the
+CUDA extension imported by src/model/modulated_deform_conv_func.py:13; the
+offset branch calls it, so offset-mode forward is NOT generated — the reference
+has no CPU DCN and its CUDA extension cannot be built here).  Nothing on the
+generated paths is substituted.
+
+Outputs: tests/golden/*.npz (float32, allow_pickle=False) + manifest.json.
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF_SRC = "/root/reference/src"
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+SEED = 7240  # the reference's default seed, src/config.py:58-61
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("torchvision", types.ModuleType("torchvision"))
+    sys.modules.setdefault("DCN", types.ModuleType("DCN"))
+    sys.path.insert(0, REF_SRC)
+    from model import nlspnmodel  # noqa: E402
+    return nlspnmodel
+
+
+def make_model(nlspnmodel, *, prop_kernel=3, affinity="TGASS", affinity_gamma=0.5,
+               prop_time=18, preserve_input=True, always_clip=False, conf_prop=True,
+               offset=False):
+    """Instance of the reference NLSPNModel with only the propagation state
+    (constants of nlspnmodel.py:29-32, :88-121), no encoder weights."""
+    args = types.SimpleNamespace(
+        prop_kernel=prop_kernel, affinity=affinity, affinity_gamma=affinity_gamma,
+        prop_time=prop_time, preserve_input=preserve_input, always_clip=always_clip,
+        conf_prop=conf_prop, offset=offset, use_GRU=False, use_S2D=False, max_depth=10.0)
+    M = nlspnmodel.NLSPNModel
+    m = M.__new__(M)
+    nn.Module.__init__(m)
+    m.args = args
+    m.num_neighbors = prop_kernel * prop_kernel - 1
+    m.ch_f = 1
+    m.idx_ref = m.num_neighbors // 2
+    if affinity == "TC":
+        m.aff_scale_const = nn.Parameter(m.num_neighbors * torch.ones(1), requires_grad=False)
+    elif affinity == "TGASS":
+        m.aff_scale_const = nn.Parameter(affinity_gamma * m.num_neighbors * torch.ones(1))
+    else:
+        m.aff_scale_const = nn.Parameter(torch.ones(1), requires_grad=False)
+    m.w = nn.Parameter(torch.ones((1, 1, prop_kernel, prop_kernel)), requires_grad=False)
+    m.b = nn.Parameter(torch.zeros(1), requires_grad=False)
+    m.stride, m.padding, m.dilation = 1, (prop_kernel - 1) // 2, 1
+    m.groups, m.deformable_groups, m.im2col_step = 1, 1, 64
+    return m
+
+
+def run_forward(m, pred_init, dep, off_aff, confidence):
+    """Run the reference forward() with the CNN heads replaced by constants."""
+    B, _, H, W = dep.shape
+    z = torch.zeros(B, 1, H, W)
+    const = lambda *a, **k: z  # noqa: E731
+    for name in ("conv1_rgb", "conv1_dep", "S2D", "conv2", "conv3", "conv4", "conv5",
+                 "dec4", "dec3", "dec2", "id_dec1", "off_aff_dec1", "cf_dec1"):
+        object.__setattr__(m, name, const)
+    object.__setattr__(m, "id_dec0", lambda *a: pred_init)
+    object.__setattr__(m, "off_aff_dec0", lambda *a: off_aff)
+    object.__setattr__(m, "cf_dec0", lambda *a: confidence)
+    with torch.no_grad():
+        return m.forward({"rgb": torch.zeros(B, 3, H, W), "dep": dep})
+
+
+def synth(g, B, H, W, K, *, density=0.05, max_depth=10.0, signed_aff=False, offset=False):
+    """Synthetic inputs: pred_init~U(0,max), dep=U(0,max)*Bern(rho),
+    conf~U(0,1), raw affinity |N(0,1)| (convex) or N(0,1), offsets N(0,2^2)."""
+    pred_init = torch.rand(B, 1, H, W, generator=g) * max_depth
+    dep = torch.rand(B, 1, H, W, generator=g) * max_depth
+    dep = dep * (torch.rand(B, 1, H, W, generator=g) < density).float()
+    conf = torch.rand(B, 1, H, W, generator=g)
+    aff = torch.randn(B, K, H, W, generator=g)
+    if not signed_aff:
+        aff = aff.abs()
+    if offset:
+        off = torch.randn(B, 2 * K, H, W, generator=g) * 2.0
+        off_aff = torch.cat([off, aff], 1)
+    else:
+        off_aff = aff
+    return pred_init, dep, conf, off_aff
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=OUT_DIR)
+    a = ap.parse_args()
+    nl = import_reference()
+    torch.set_num_threads(1)
+    manifest = {"generator": "tests/golden/gen_golden.py", "seed": SEED,
+                "reference": "XJTUXYC/NLSPN_ECCV20 src/model/nlspnmodel.py", "cases": {}}
+    g = torch.Generator().manual_seed(SEED)
+
+    def save(name, desc, **arrs):
+        path = os.path.join(a.out, name + ".npz")
+        np.savez_compressed(path, **{k: np.ascontiguousarray(v.detach().numpy() if torch.is_tensor(v) else v)
+                                     for k, v in arrs.items()})
+        manifest["cases"][name] = {"desc": desc, "arrays": {k: list(np.shape(v)) for k, v in arrs.items()}}
+
+    # 1) affinity normalisation (:179-201 + :261-269), all kinds, K=8 and K=24.
+    for kind in ("AS", "ASS", "TC", "TGASS"):
+        for pk in (3, 5):
+            m = make_model(nl, prop_kernel=pk, affinity=kind)
+            K = m.num_neighbors
+            raw = torch.randn(2, K, 6, 10, generator=g) * 2.0
+            raw[:, :, :3] *= 0.02           # small rows: exercise the s<1 clamp (ASS/TGASS)
+            raw[0, :, 5, 9] = 0.0           # all-zero pixel: taps [0..1..0]
+            with torch.no_grad():
+                out = m._affinity_normalization(raw)
+            save(f"affnorm_{kind}_k{K}", f"_affinity_normalization kind={kind} prop_kernel={pk}",
+                 aff_raw=raw, gamma=m.aff_scale_const.detach().reshape(1), aff=out)
+
+    # 2) _off_insert (:252-259)
+    m = make_model(nl, prop_kernel=3)
+    off = torch.randn(2, 16, 5, 7, generator=g)
+    save("off_insert_k8", "_off_insert prop_kernel=3", off_raw=off, offset=m._off_insert(off))
+
+    # 3) one no-offset step (:209-224)
+    feat = torch.rand(2, 1, 9, 13, generator=g) * 10
+    raw = torch.randn(2, 8, 9, 13, generator=g).abs()
+    with torch.no_grad():
+        aff = m._affinity_normalization(raw)
+        out = m._propagate_once(feat, None, aff)
+    save("step_noffset", "_propagate_once(feat, None, aff) 3x3 replicate", feat=feat, aff=aff, out=out)
+
+    # 4) full forward propagation section (:317-383), no-offset branch, T=18.
+    cases = [
+        ("loop_tgass_preserve", dict(affinity="TGASS", preserve_input=True, always_clip=False, conf_prop=True)),
+        ("loop_tgass_clip", dict(affinity="TGASS", preserve_input=True, always_clip=True, conf_prop=True)),
+        ("loop_tgass_noconf", dict(affinity="TGASS", preserve_input=True, always_clip=False, conf_prop=False)),
+        ("loop_tgass_nopreserve", dict(affinity="TGASS", preserve_input=False, always_clip=False, conf_prop=True)),
+        ("loop_ass_preserve", dict(affinity="ASS", preserve_input=True, always_clip=False, conf_prop=True)),
+        ("loop_tc_preserve", dict(affinity="TC", preserve_input=True, always_clip=True, conf_prop=True)),
+        ("loop_as_preserve", dict(affinity="AS", preserve_input=True, always_clip=False, conf_prop=True)),
+    ]
+    B, H, W = 2, 16, 24
+    for name, kw in cases:
+        m = make_model(nl, prop_kernel=3, prop_time=18, **kw)
+        pred_init, dep, conf, off_aff = synth(g, B, H, W, 8)
+        o = run_forward(m, pred_init, dep, off_aff, conf if kw["conf_prop"] else None)
+        arrs = dict(pred_init=pred_init, dep=dep, aff_raw=off_aff,
+                    gamma=m.aff_scale_const.detach().reshape(1),
+                    pred=o["pred"], pred_inter=torch.stack(o["pred_inter"], 0), aff=o["aff"])
+        if kw["conf_prop"]:
+            arrs.update(conf=conf, confidence=o["confidence"])
+        save(name, f"forward propagation section, no offset, T=18, {kw}", **arrs)
+
+    # 5) a larger loop at the survey's suggested fixture size, final pred only.
+    m = make_model(nl, prop_kernel=3, prop_time=18)
+    pred_init, dep, conf, off_aff = synth(g, 1, 40, 56, 8, density=0.02)
+    o = run_forward(m, pred_init, dep, off_aff, conf)
+    save("loop_tgass_40x56", "forward propagation section, no offset, T=18, 1x40x56",
+         pred_init=pred_init, dep=dep, conf=conf, aff_raw=off_aff,
+         gamma=m.aff_scale_const.detach().reshape(1), pred=o["pred"],
+         pred_inter_last=o["pred_inter"][-1], confidence=o["confidence"])
+
+    with open(os.path.join(a.out, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    total = sum(os.path.getsize(os.path.join(a.out, n + ".npz")) for n in manifest["cases"])
+    print(f"wrote {len(manifest['cases'])} fixtures, {total/1024:.1f} KiB")
+
+
+if __name__ == "__main__":
+    main()
