@@ -74,6 +74,88 @@ template <> struct Vec<__half, 4> {
     }
 };
 
+// ---- raw buffer access (cdna_hip_programming.md §5.5 T8): one wave-uniform
+// descriptor per batch item, a 32-bit per-lane byte offset shared by every plane,
+// and the plane offset in an SGPR (soffset).  Compared with flat 64-bit
+// per-lane addresses this frees ~2 VGPRs per in-flight plane.  num_records is
+// the 2 GiB maximum: each descriptor spans one batch item's planes (host checks).
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// NOTE (hipcc / ROCm 7.2, gfx950): extracting elements of a raw_buffer_load_b64/
+// b96/b128 result one by one with __builtin_bit_cast(float, q[i]) miscompiles —
+// the load is narrowed to a single dword while the other lanes of the vector are
+// still read (garbage).  Bit-cast the WHOLE vector to a float/half vector first;
+// that form emits buffer_load_dwordx2/x4 correctly.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T, int PX> struct BVec;
+
+template <> struct BVec<float, 1> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[1]) {
+        v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[1]) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), r, vo, so, 0);
+    }
+};
+template <> struct BVec<float, 2> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[2]) {
+        const f32x2 q = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+        v[0] = q[0]; v[1] = q[1];
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[2]) {
+        const f32x2 q = {v[0], v[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, 0);
+    }
+};
+template <> struct BVec<float, 4> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[4]) {
+        const f32x4 q = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
+        const f32x4 q = {v[0], v[1], v[2], v[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q), r, vo, so, 0);
+    }
+};
+template <> struct BVec<__half, 1> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[1]) {
+        v[0] = (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0));
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[1]) {
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v[0]), r, vo, so, 0);
+    }
+};
+template <> struct BVec<__half, 2> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[2]) {
+        const f16x2 q = __builtin_bit_cast(f16x2, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+        v[0] = (float)q[0]; v[1] = (float)q[1];
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[2]) {
+        const f16x2 q = {(_Float16)v[0], (_Float16)v[1]};
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, q), r, vo, so, 0);
+    }
+};
+template <> struct BVec<__half, 4> {
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[4]) {
+        const f16x4 q = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+        v[0] = (float)q[0]; v[1] = (float)q[1]; v[2] = (float)q[2]; v[3] = (float)q[3];
+    }
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
+        const f16x4 q = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, 0);
+    }
+};
+
 // torch.clamp(x, min=0) (NaN propagates).
 __device__ __forceinline__ float clamp0(float v) { return v < 0.f ? 0.f : v; }
 

@@ -8,15 +8,18 @@
 //   preserve-input blend + optional clamp         (:355-361)   [+ final clamp :375-377 on the last]
 // with one launch, no `columns` buffer and no GEMM (the NLSPN weight is all ones).
 //
-// Structure (one 256-thread workgroup per TH x TW output tile, PX pixels per thread):
-//   1. issue the tile's streamed loads first — K normalised-affinity planes,
-//      2K offset planes and dep — 16-B (fp32) / 8-B (fp16) per lane, coalesced;
+// Structure (one workgroup per TH x TW output tile, PX pixels per thread):
+//   1. issue the window's staging loads (p_in, conf; clamped, branch-free), then
+//      the tile's streamed loads — K normalised-affinity planes, 2K offset planes
+//      and dep — 16-B (fp32) / 8-B (fp16) per lane, coalesced;
 //   2. stage f = p_in * conf for the tile + halo window into LDS (fp32), zero
 //      outside the image (= the reference's zero-padded bilinear) or replicate-
-//      clamped for the no-offset branch;
+//      clamped for the no-offset branch; an LDS-only barrier keeps the streamed
+//      loads in flight;
 //   3. per tap, bilinear-sample f from LDS; taps whose 2x2 footprint leaves the
-//      window (learned offsets are unbounded) fall back to L2/global reads with
-//      the reference's per-corner checks — correctness never depends on HALO;
+//      window (learned offsets are unbounded) are flagged and served afterwards
+//      from L2/global with the reference's per-corner checks — correctness never
+//      depends on the halo;
 //   4. accumulate taps in index order with the reference tap (index K/2) weighted
 //      1 - sum(others); blend, clamp, store p_out (and pred on the last step).
 // Summation and bilinear arithmetic follow the reference's operation order; the
@@ -47,16 +50,37 @@ struct StepArgs {
 constexpr unsigned kPreserve = 0x1u;
 constexpr unsigned kAlwaysClip = 0x2u;
 
+// f = p * conf at pixel q of the batch item (buffer loads; conf may be absent)
 template <typename T>
-__device__ __forceinline__ float fetch_f(const T *__restrict__ pin, const T *__restrict__ cf, long long q) {
-    float v = ld(pin + q);
-    if (cf) v = v * ld(cf + q);
-    return v;
+__device__ __forceinline__ float fetch_f(rsrc_t rp, rsrc_t rc, bool has_conf, unsigned q) {
+    float v[1];
+    BVec<T, 1>::load(rp, q * (unsigned)sizeof(T), 0u, v);
+    if (has_conf) {
+        float c[1];
+        BVec<T, 1>::load(rc, q * (unsigned)sizeof(T), 0u, c);
+        return v[0] * c[0];
+    }
+    return v[0];
+}
+
+// Workgroup barrier that orders LDS only (no global-memory release): it waits
+// lgkmcnt(0) but leaves the streamed global loads in flight across the barrier,
+// so their latency overlaps staging and the first taps (the full __syncthreads
+// fence would drain vmcnt(0) here and serialise load and compute phases).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // KH x KW taps; TH x TW tile; PX px per thread; window radii RY/RX; SV = staging
 // vector width (4 requires W % 4 == 0 and RX % 4 == 0); PRE = preload offsets
 // before the staging barrier.
+//
+// Load order matters (s_waitcnt vmcnt counts in issue order): the window's
+// staging loads go out FIRST with clamped, branch-free addresses, then the
+// streamed per-pixel planes; staging waits only for its own loads
+// (vmcnt(#streamed)), and each tap waits only for the planes it consumes.
 template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE>
 __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     constexpr int NT = TH * TW / PX;
@@ -67,7 +91,10 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     static_assert(TW % PX == 0 && NT % 64 == 0, "tile/thread shape");
     static_assert(OFFSET || (KH == 3 && KW == 3 && RY == 1 && RX == 1), "no-offset branch is 3x3 replicate");
     static_assert(!OFFSET || (RY > PH && RX > PW), "window must cover the tap base grid");
-    static_assert(SV == 1 || (RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
+    static_assert(SV == 1 || (OFFSET && RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
+    constexpr int WV = WW / SV;                  // staging vectors per window row
+    constexpr int NV = WH * WV;                  // staging vectors per window
+    constexpr int SIT = (NV + NT - 1) / NT;      // staging vectors per thread
     __shared__ __attribute__((aligned(16))) float win[WH * WW];
 
     const int H = a.H, W = a.W;
@@ -80,150 +107,192 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     const int x0 = tx * TW, y0 = ty * TH;
     const int wy0 = y0 - RY, wx0 = x0 - RX;
 
-    const T *__restrict__ pin = static_cast<const T *>(a.p_in) + b * HW;
-    const T *__restrict__ cf = a.conf ? static_cast<const T *>(a.conf) + b * HW : nullptr;
+    constexpr unsigned ES = sizeof(T);
+    const bool has_conf = a.conf != nullptr;
+    const rsrc_t rp = make_rsrc(static_cast<const T *>(a.p_in) + b * HW);
+    const rsrc_t rc = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : static_cast<const T *>(a.p_in));
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
 
     const int ly = threadIdx.x / TPR, lx = (threadIdx.x % TPR) * PX;
     const int y = y0 + ly, xb = x0 + lx;
     const bool active = (y < H) && (xb < W);  // PX>1 requires W % PX == 0: groups are all-in or all-out
-    const long long pix = (long long)y * W + xb;
+    // Per-lane offsets are 32-bit (a plane holds < 2^31 pixels); plane bases are
+    // wave-uniform, so loads take the saddr + 32-bit voffset form (fewer VGPRs).
+    const unsigned pix = active ? (unsigned)(y * W + xb) : 0u;  // inactive lanes load pixel 0 (in bounds)
 
-    // ---- 1. streamed per-pixel loads (issued before staging so they overlap it)
-    float av[K][PX];
+    // ---- 1. staging loads (first): f = p * conf over the window, clamped addresses
+    float sp[SIT][SV], sc[SIT][SV];
+    bool sin[SIT];
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+        const int i = threadIdx.x + it * NT;
+        const int ii = i < NV ? i : NV - 1;
+        const int r = ii / WV, c = (ii - r * WV) * SV;
+        int gy = wy0 + r, gx = wx0 + c;
+        if (OFFSET) {
+            sin[it] = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;   // zero padding outside
+        } else {
+            sin[it] = i < NV;                                              // replicate padding
+        }
+        gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
+        gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
+        const unsigned q = (unsigned)(gy * W + gx) * ES;
+        BVec<T, SV>::load(rp, q, 0u, sp[it]);
+        if (has_conf) BVec<T, SV>::load(rc, q, 0u, sc[it]);
+    }
+
+    // ---- 2. streamed per-pixel loads: K affinity planes, 2K offset planes, dep.
+    // PRE (small K): all issued now, before the staging barrier; otherwise each
+    // tap's planes are loaded inside pass A below.
+    float av[PRE ? K : 1][PX];
     float dh[PRE ? K : 1][PX], dw[PRE ? K : 1][PX];
     float dv[PX];
-    const T *__restrict__ offb = nullptr;
-    if (active) {
-        const T *__restrict__ ab = static_cast<const T *>(a.aff) + b * a.aff_bs + pix;
+    const rsrc_t ra = make_rsrc(static_cast<const T *>(a.aff) + b * a.aff_bs);
+    const rsrc_t ro = make_rsrc(OFFSET ? static_cast<const T *>(a.off) + b * a.off_bs : static_cast<const T *>(a.aff));
+    const unsigned vpix = pix * ES;            // per-lane byte offset, shared by every plane
+    const unsigned plane_bytes = (unsigned)HW * ES;
+    if (PRE) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) Vec<T, PX>::load(ab + (long long)(k < REF ? k : k + 1) * HW, av[k]);
-        if (OFFSET) {
-            offb = static_cast<const T *>(a.off) + b * a.off_bs + pix;
-            if (PRE) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int c = a.off_raw ? k : (k < REF ? k : k + 1);
-                    Vec<T, PX>::load(offb + (long long)(2 * c) * HW, dh[PRE ? k : 0]);
-                    Vec<T, PX>::load(offb + (long long)(2 * c + 1) * HW, dw[PRE ? k : 0]);
-                }
+        for (int k = 0; k < K; ++k) {
+            BVec<T, PX>::load(ra, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, av[PRE ? k : 0]);
+            if (OFFSET) {
+                const unsigned c = a.off_raw ? k : (k < REF ? k : k + 1);
+                BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, dh[PRE ? k : 0]);
+                BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, dw[PRE ? k : 0]);
             }
         }
-        if (preserve) Vec<T, PX>::load(static_cast<const T *>(a.dep) + b * HW + pix, dv);
     }
+    if (preserve) BVec<T, PX>::load(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
 
-    // ---- 2. stage f = p * conf over the window
-    if (OFFSET) {
-        if (SV == 4) {
-            constexpr int WW4 = WW / 4;
-            for (int i = threadIdx.x; i < WH * WW4; i += NT) {
-                const int r = i / WW4, c4 = (i - r * WW4) * 4;
-                const int gy = wy0 + r, gx = wx0 + c4;
-                float v[4] = {0.f, 0.f, 0.f, 0.f};
-                if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-                    const long long q = (long long)gy * W + gx;
-                    Vec<T, 4>::load(pin + q, v);
-                    if (cf) {
-                        float c[4];
-                        Vec<T, 4>::load(cf + q, c);
+    // ---- 3. finish staging into LDS (waits for the staging loads only)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = v[e] * c[e];
-                    }
-                }
-                *reinterpret_cast<float4 *>(&win[r * WW + c4]) = make_float4(v[0], v[1], v[2], v[3]);
+    for (int it = 0; it < SIT; ++it) {
+        const int i = threadIdx.x + it * NT;
+        if (i < NV) {
+            float v[SV];
+#pragma unroll
+            for (int e = 0; e < SV; ++e) {
+                const float f = has_conf ? sp[it][e] * sc[it][e] : sp[it][e];
+                v[e] = sin[it] ? f : 0.f;
             }
-        } else {
-            for (int i = threadIdx.x; i < WH * WW; i += NT) {
-                const int r = i / WW, c = i - r * WW;
-                const int gy = wy0 + r, gx = wx0 + c;
-                float v = 0.f;
-                if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = fetch_f(pin, cf, (long long)gy * W + gx);
-                win[i] = v;
-            }
-        }
-    } else {
-        // F.pad(feat, (1,1,1,1), mode="replicate") (nlspnmodel.py:210)
-        for (int i = threadIdx.x; i < WH * WW; i += NT) {
-            const int r = i / WW, c = i - r * WW;
-            int gy = wy0 + r, gx = wx0 + c;
-            gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
-            gx = gx < 0 ? 0 : (gx > W - 1 ? W - 1 : gx);
-            win[i] = fetch_f(pin, cf, (long long)gy * W + gx);
+            const int r = i / WV, c = (i - r * WV) * SV;
+            if constexpr (SV == 4)
+                *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
+            else
+                win[r * WW + c] = v[0];
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (!active) return;  // no barrier below
 
-    // ---- 3. taps, in index order; reference tap weight = 1 - sum(others) (nlspnmodel.py:262-263)
-    float aref[PX], acc[PX];
+    // ---- 4. taps.  Pass A (LDS only, no divergent global loads, so the
+    // compiler's vmcnt waits stay counted per tap): col[k] = bilinear * a_k for
+    // every tap whose 2x2 footprint is inside the window; out-of-window taps are
+    // flagged in `fb`.  Pass B (rare): flagged taps from L2/global with the
+    // reference's per-corner checks (their offsets/affinity re-read from cache).
+    // Then accumulate in tap index order with the reference tap (K/2) weighted
+    // 1 - sum(others) (nlspnmodel.py:262-263): the reference's summation order,
+    // whichever pass served a tap.  col = val * a then acc += col is the same
+    // IEEE sequence as acc += val * a (no contraction).
+    float col[K][PX], asum[PX];
 #pragma unroll
-    for (int p = 0; p < PX; ++p) {
-        float s = 0.f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) s += av[k][p];
-        aref[p] = 1.0f - s;
-        acc[p] = 0.f;
-    }
+    for (int p = 0; p < PX; ++p) asum[p] = 0.f;
     const float Hf = (float)H, Wf = (float)W;
+    constexpr int NFB = (K * PX + 31) / 32;
+    uint32_t fb[NFB];
 #pragma unroll
-    for (int t = 0; t < KK; ++t) {
+    for (int q = 0; q < NFB; ++q) fb[q] = 0u;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int t = k < REF ? k : k + 1;
         const int i = t / KW, j = t % KW;
-        if (t == REF) {
-            // zero offset, integer sample point: the bilinear weight is exactly (1,0,0,0)
-#pragma unroll
-            for (int p = 0; p < PX; ++p) acc[p] += win[(ly + RY) * WW + lx + p + RX] * aref[p];
-            continue;
-        }
-        const int k = t < REF ? t : t - 1;
-        if (!OFFSET) {
-#pragma unroll
-            for (int p = 0; p < PX; ++p) acc[p] += win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * av[k][p];
-            continue;
-        }
-        float tdh[PX], tdw[PX];
+        float ak[PX], tdh[PX], tdw[PX];
         if (PRE) {
 #pragma unroll
-            for (int p = 0; p < PX; ++p) { tdh[p] = dh[PRE ? k : 0][p]; tdw[p] = dw[PRE ? k : 0][p]; }
+            for (int p = 0; p < PX; ++p) {
+                ak[p] = av[PRE ? k : 0][p];
+                tdh[p] = dh[PRE ? k : 0][p];
+                tdw[p] = dw[PRE ? k : 0][p];
+            }
         } else {
-            const int c = a.off_raw ? k : t;
-            Vec<T, PX>::load(offb + (long long)(2 * c) * HW, tdh);
-            Vec<T, PX>::load(offb + (long long)(2 * c + 1) * HW, tdw);
+            BVec<T, PX>::load(ra, vpix, (unsigned)t * plane_bytes, ak);
+            if (OFFSET) {
+                const unsigned c = a.off_raw ? k : t;
+                BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, tdh);
+                BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, tdw);
+            }
         }
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
+            asum[p] += ak[p];
+            if (!OFFSET) {
+                col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
+                continue;
+            }
             // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
             const float h_im = (float)(y - PH + i) + tdh[p];
             const float w_im = (float)(xb + p - PW + j) + tdw[p];
-            float val = 0.f;
+            float v = 0.f;
             if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                 const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
-                const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
-                const float hh = 1.f - lh, hw = 1.f - lw;
                 const int ry = h_low - wy0, rx = w_low - wx0;
-                float v1, v2, v3, v4;
                 if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
+                    const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                    const float hh = 1.f - lh, hw = 1.f - lw;
                     const float *s = &win[ry * WW + rx];
-                    v1 = s[0];
-                    v2 = s[1];
-                    v3 = s[WW];
-                    v4 = s[WW + 1];
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
                 } else {
-                    const int h_high = h_low + 1, w_high = w_low + 1;
-                    const long long r0 = (long long)h_low * W, r1 = (long long)h_high * W;
-                    v1 = (h_low >= 0 && w_low >= 0) ? fetch_f(pin, cf, r0 + w_low) : 0.f;
-                    v2 = (h_low >= 0 && w_high <= W - 1) ? fetch_f(pin, cf, r0 + w_high) : 0.f;
-                    v3 = (h_high <= H - 1 && w_low >= 0) ? fetch_f(pin, cf, r1 + w_low) : 0.f;
-                    v4 = (h_high <= H - 1 && w_high <= W - 1) ? fetch_f(pin, cf, r1 + w_high) : 0.f;
+                    fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);
                 }
-                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                val = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
             }
-            acc[p] += val * av[k][p];
+            col[k][p] = v * ak[p];  // .cuh:189 col = val * mask
         }
     }
+    uint32_t any_fb = 0u;
+#pragma unroll
+    for (int q = 0; q < NFB; ++q) any_fb |= fb[q];
+    if (OFFSET && any_fb) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = k < REF ? k : k + 1;
+            const int i = t / KW, j = t % KW;
+#pragma unroll
+            for (int p = 0; p < PX; ++p) {
+                if (!(fb[(k * PX + p) >> 5] & (1u << ((k * PX + p) & 31)))) continue;
+                const unsigned c = a.off_raw ? k : t;
+                float o1[1], a1[1];
+                BVec<T, 1>::load(ro, vpix + p * ES, (2 * c) * plane_bytes, o1);
+                const float h_im = (float)(y - PH + i) + o1[0];
+                BVec<T, 1>::load(ro, vpix + p * ES, (2 * c + 1) * plane_bytes, o1);
+                const float w_im = (float)(xb + p - PW + j) + o1[0];
+                BVec<T, 1>::load(ra, vpix + p * ES, (unsigned)t * plane_bytes, a1);
+                const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                const int h_high = h_low + 1, w_high = w_low + 1;
+                const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                const float hh = 1.f - lh, hw = 1.f - lw;
+                const int r0 = h_low * W, r1 = h_high * W;
+                const float v1 = (h_low >= 0 && w_low >= 0) ? fetch_f<T>(rp, rc, has_conf, r0 + w_low) : 0.f;
+                const float v2 = (h_low >= 0 && w_high <= W - 1) ? fetch_f<T>(rp, rc, has_conf, r0 + w_high) : 0.f;
+                const float v3 = (h_high <= H - 1 && w_low >= 0) ? fetch_f<T>(rp, rc, has_conf, r1 + w_low) : 0.f;
+                const float v4 = (h_high <= H - 1 && w_high <= W - 1) ? fetch_f<T>(rp, rc, has_conf, r1 + w_high) : 0.f;
+                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                col[k][p] = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4) * a1[0];
+            }
+        }
+    }
+    float acc[PX];
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+        // reference tap: zero offset, integer sample point -> bilinear weight exactly (1,0,0,0)
+        const float cref = win[(ly + RY) * WW + lx + p + RX] * (1.0f - asum[p]);
+        acc[p] = 0.f;
+#pragma unroll
+        for (int t = 0; t < KK; ++t) acc[p] += t == REF ? cref : col[t < REF ? t : t - 1][p];
+    }
 
-    // ---- 4. preserve-input blend (:355-357), clamp (:359-361), final clamp (:375-377)
+    // ---- 5. preserve-input blend (:355-357), clamp (:359-361), final clamp (:375-377)
     float o[PX], fin[PX];
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
@@ -236,8 +305,8 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
         o[p] = v;
         fin[p] = clip ? v : clamp0(v);
     }
-    Vec<T, PX>::store(static_cast<T *>(a.p_out) + b * HW + pix, o);
-    if (a.pred_out) Vec<T, PX>::store(static_cast<T *>(a.pred_out) + b * HW + pix, fin);
+    BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.p_out) + b * HW), vpix, 0u, o);
+    if (a.pred_out) BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.pred_out) + b * HW), vpix, 0u, fin);
 }
 
 }  // namespace nlspn
