@@ -97,22 +97,23 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
                     void *p_out, void *pred_out,
                     int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
 
-/* Bytes of device workspace nlspn_propagate needs (one plane per batch item). */
+/* Bytes of device workspace nlspn_propagate needs (currently 0: the prologue is
+ * fused into the first iteration; the argument is kept for ABI stability). */
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
 
 /*
- * The whole propagation section, src/model/nlspnmodel.py:323-381, as
- * 1 prologue launch + T iteration launches:
- *   prologue : _off_insert (:324) if off_out, _affinity_normalization (:325),
- *              mask_fix / confidence blend (:328-334), first blend+clamp (:341-348)
- *   T steps  : nlspn_prop_step, writing pred_inter[t]; the last also writes pred.
+ * The whole propagation section, src/model/nlspnmodel.py:323-381, as T launches:
+ *   step 1   : the prologue fused into the first iteration — _off_insert (:324)
+ *              if off_out, _affinity_normalization (:325), mask_fix / confidence
+ *              blend (:328-334), first blend+clamp (:341-348), then iteration 1
+ *   steps 2..T: nlspn_prop_step, writing pred_inter[t]; the last also writes pred.
  * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
  *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
  *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
  * Outputs: pred_inter (T x B planes, contiguous: list_pred), pred (B planes),
  *          aff_out (B x (K+1) planes), off_out (B x 2(K+1) planes, optional),
  *          conf_out (B planes, required iff conf != NULL).
- * workspace: nlspn_workspace_bytes() bytes of device memory.
+ * workspace: nlspn_workspace_bytes() bytes of device memory (may be NULL when 0).
  */
 int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
                     const void *aff_raw, int64_t aff_bstride,
@@ -123,9 +124,9 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
                     unsigned flags, void *stream);
 
 /*
- * Graph plans: nlspn_propagate captured once into a hipGraph (1 + T kernel
- * nodes) and replayed with one hipGraphLaunch.  Pointers are baked in at
- * creation; γ stays live because it is read from device memory.
+ * Graph plans: nlspn_propagate captured once into a hipGraph (T kernel nodes)
+ * and replayed with one hipGraphLaunch.  Pointers are baked in at creation;
+ * γ stays live because it is read from device memory.
  */
 typedef struct nlspn_plan *nlspn_plan_t;
 int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep,

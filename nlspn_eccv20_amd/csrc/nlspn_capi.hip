@@ -12,7 +12,7 @@
 
 #include "../../include/nlspn_prop.h"
 #include "nlspn_mdcn.h"
-#include "nlspn_prologue.h"
+#include "nlspn_affnorm.h"
 #include "nlspn_step.h"
 
 using namespace nlspn;
@@ -56,9 +56,10 @@ struct StepLaunch {
 };
 
 template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE>
-StepLaunch make_step(StepArgs &a) {
+StepLaunch make_step(StepArgs &a, bool first) {
     StepLaunch L;
-    L.fn = reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, OFFSET, PRE>);
+    L.fn = first ? reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, OFFSET, PRE, true>)
+                 : reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, OFFSET, PRE, false>);
     a.tiles_x = (a.W + TW - 1) / TW;
     a.tiles_y = (a.H + TH - 1) / TH;
     L.grid = dim3((unsigned)(a.B * a.tiles_x * a.tiles_y));
@@ -66,33 +67,32 @@ StepLaunch make_step(StepArgs &a) {
     return L;
 }
 
-// Tile configurations per geometry.  vec: 16-B (fp32) / 8-B (fp16) lane loads,
-// needs W % 4 == 0 and aligned planes; scalar: any shape.
+// Tile configurations per geometry.  vec: 16-B staging loads, needs W % 4 == 0
+// and aligned planes; scalar: any shape.  Tiles measured with tools/step_bench
+// (interleaved A/B, dispatch events): one pixel per lane and small 8x32 tiles
+// keep the kernel at the streaming ceiling of its 4+3K planes.
 template <typename T>
-int select_step(StepArgs &a, int kh, int kw, bool offset, bool vec, StepLaunch &L) {
+int select_step(StepArgs &a, int kh, int kw, bool offset, bool vec, bool first, StepLaunch &L) {
     if (!offset) {
         if (kh != 3 || kw != 3)
             return fail(NLSPN_EUNSUPPORTED,
                         "no-offset propagation is 3x3 replicate (nlspnmodel.py:209-224); got %dx%d", kh, kw);
-        L = vec ? make_step<T, 3, 3, 16, 64, 4, 1, 1, 1, false, false>(a)
-                : make_step<T, 3, 3, 4, 64, 1, 1, 1, 1, false, false>(a);
+        L = vec ? make_step<T, 3, 3, 16, 64, 4, 1, 1, 1, false, true>(a, first)
+                : make_step<T, 3, 3, 4, 64, 1, 1, 1, 1, false, true>(a, first);
         return NLSPN_OK;
     }
-    // Tiles measured with tools/step_bench (interleaved A/B, dispatch events): one
-    // pixel per lane and small 8x32 tiles keep the kernel at the streaming ceiling
-    // of its 4+3K planes (C2 11.2 us, C3 20.1 us per iteration on MI355X).
     if (kh == 3 && kw == 3)
-        L = vec ? make_step<T, 3, 3, 8, 32, 1, 8, 8, 4, true, true>(a)
-                : make_step<T, 3, 3, 4, 64, 1, 8, 8, 1, true, true>(a);
+        L = vec ? make_step<T, 3, 3, 8, 32, 1, 8, 8, 4, true, true>(a, first)
+                : make_step<T, 3, 3, 4, 64, 1, 8, 8, 1, true, true>(a, first);
     else if (kh == 1 && kw == 17)
-        L = vec ? make_step<T, 1, 17, 8, 32, 1, 8, 16, 4, true, true>(a)
-                : make_step<T, 1, 17, 4, 64, 1, 8, 16, 1, true, true>(a);
+        L = vec ? make_step<T, 1, 17, 8, 32, 1, 8, 16, 4, true, true>(a, first)
+                : make_step<T, 1, 17, 4, 64, 1, 8, 16, 1, true, true>(a, first);
     else if (kh == 5 && kw == 5)
-        L = vec ? make_step<T, 5, 5, 8, 32, 1, 8, 8, 4, true, true>(a)
-                : make_step<T, 5, 5, 4, 64, 1, 8, 8, 1, true, true>(a);
+        L = vec ? make_step<T, 5, 5, 8, 32, 1, 8, 8, 4, true, true>(a, first)
+                : make_step<T, 5, 5, 4, 64, 1, 8, 8, 1, true, true>(a, first);
     else if (kh == 7 && kw == 7)
-        L = vec ? make_step<T, 7, 7, 8, 32, 1, 8, 8, 4, true, true>(a)
-                : make_step<T, 7, 7, 4, 64, 1, 8, 8, 1, true, true>(a);
+        L = vec ? make_step<T, 7, 7, 8, 32, 1, 8, 8, 4, true, true>(a, first)
+                : make_step<T, 7, 7, 4, 64, 1, 8, 8, 1, true, true>(a, first);
     else
         return fail(NLSPN_EUNSUPPORTED, "no kernel instantiation for a %dx%d propagation geometry "
                     "(supported: 3x3, 5x5, 7x7, 1x17)", kh, kw);
@@ -103,6 +103,7 @@ struct StepReq {
     int dtype;
     StepArgs a;
     int kh, kw;
+    bool first = false;  // fused-prologue first iteration
 };
 
 int prepare_step(StepReq &r, StepLaunch &L) {
@@ -116,7 +117,10 @@ int prepare_step(StepReq &r, StepLaunch &L) {
     if ((a.flags & kPreserve) && !a.dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
     const long long HW = (long long)a.H * a.W;
     const int K = r.kh * r.kw - 1;
-    if (a.aff_bs < (long long)(K + 1) * HW) return fail(NLSPN_EINVAL, "aff batch stride %lld < (K+1)*H*W", a.aff_bs);
+    const long long aplanes = r.first ? K : K + 1;
+    if (a.aff_bs < aplanes * HW) return fail(NLSPN_EINVAL, "aff batch stride %lld < %lld*H*W", a.aff_bs, aplanes);
+    if ((long long)HW * (3LL * K + 4) * (long long)esize(r.dtype) > 0x7fffffffLL)
+        return fail(NLSPN_EINVAL, "image too large: one batch item's planes must stay below 2 GiB");
     if (a.off) {
         const long long need = (long long)(a.off_raw ? 2 * K : 2 * (K + 1)) * HW;
         if (a.off_bs < need) return fail(NLSPN_EINVAL, "offset batch stride %lld < %lld", a.off_bs, need);
@@ -124,11 +128,11 @@ int prepare_step(StepReq &r, StepLaunch &L) {
     if ((long long)a.B * ((a.H + 3) / 4) * ((a.W + 63) / 64) > 0x7fffffffLL)
         return fail(NLSPN_EINVAL, "grid too large");
     const size_t vb = 4 * esize(r.dtype);
-    const bool vec = (a.W % 4 == 0) && (a.aff_bs % 4 == 0) && (!a.off || a.off_bs % 4 == 0) &&
-                     aligned(a.p_in, vb) && aligned(a.conf, vb) && aligned(a.dep, vb) && aligned(a.aff, vb) &&
-                     aligned(a.off, vb) && aligned(a.p_out, vb) && aligned(a.pred_out, vb);
-    return r.dtype == NLSPN_DTYPE_F32 ? select_step<float>(a, r.kh, r.kw, a.off != nullptr, vec, L)
-                                      : select_step<__half>(a, r.kh, r.kw, a.off != nullptr, vec, L);
+    // Element-aligned planes suffice for the 1-pixel-per-lane loads; 16-B window
+    // staging needs W % 4 == 0 and a 16-B aligned p_in / conf / dep.
+    const bool vec = (a.W % 4 == 0) && aligned(a.p_in, vb) && aligned(a.conf, vb) && aligned(a.dep, vb);
+    return r.dtype == NLSPN_DTYPE_F32 ? select_step<float>(a, r.kh, r.kw, a.off != nullptr, vec, r.first, L)
+                                      : select_step<__half>(a, r.kh, r.kw, a.off != nullptr, vec, r.first, L);
 }
 
 int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
@@ -140,23 +144,7 @@ int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = null
     return check_launch("nlspn_prop_step");
 }
 
-// ------------------------------------------------------------ prologue dispatch
-// One pixel per lane: the 4-wide variant holds all 3K+4 planes of 4 pixels in
-// registers (occupancy 1) and ran 36 us vs 21 us at C2 (tools/step_bench).
-template <typename T, int K>
-const void *prologue_fn(bool) {
-    return reinterpret_cast<const void *>(&prologue_kernel<T, K, 1>);
-}
-template <typename T>
-const void *select_prologue(int K, bool vec) {
-    switch (K) {
-        case 8: return prologue_fn<T, 8>(vec);
-        case 16: return prologue_fn<T, 16>(vec);
-        case 24: return prologue_fn<T, 24>(vec);
-        case 48: return prologue_fn<T, 48>(vec);
-        default: return nullptr;
-    }
-}
+// ------------------------------------------------------- affinity-normalisation dispatch
 template <typename T, int K>
 const void *affnorm_fn(bool vec) {
     return vec ? reinterpret_cast<const void *>(&affnorm_kernel<T, K, 4>)
@@ -215,14 +203,17 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
     r.kh = kh;
     r.kw = kw;
     r.a = StepArgs{p_in, conf, dep, aff, off, p_out, pred_out, aff_bstride, off_bstride, B, H, W, 0, 0,
-                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags};
+                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags, nullptr, nullptr, nullptr, nullptr, 0};
     StepLaunch L;
     int rc = prepare_step(r, L);
     if (rc) return rc;
     return launch(L, r.a, as_stream(stream));
 }
 
-size_t nlspn_workspace_bytes(int dtype, int B, int H, int W) { return esize(dtype) * (size_t)B * H * W; }
+size_t nlspn_workspace_bytes(int dtype, int B, int H, int W) {
+    (void)dtype; (void)B; (void)H; (void)W;
+    return 0;  // the prologue is fused into the first iteration; no scratch plane is needed
+}
 
 int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
                     int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
@@ -234,7 +225,7 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
     if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
     if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
         return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
-    if (!pred_init || !aff_raw || !gamma || !pred_inter || !pred || !aff_out || !workspace)
+    if (!pred_init || !aff_raw || !gamma || !pred_inter || !pred || !aff_out)
         return fail(NLSPN_EINVAL, "null required pointer");
     if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
     if (conf && !conf_out) return fail(NLSPN_EINVAL, "conf given without conf_out");
@@ -246,35 +237,33 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
     hipStream_t s = as_stream(stream);
     const size_t es = esize(dtype);
 
-    // validate the step configuration before launching anything
+    // iteration 1 with the prologue fused in (raw head outputs in, output-dict
+    // tensors out), then T-1 steps on the normalised affinity and conf'
+    StepReq r1{};
+    r1.dtype = dtype;
+    r1.kh = kh;
+    r1.kw = kw;
+    r1.first = true;
+    r1.a = StepArgs{pred_init, conf, dep, aff_raw, off_raw, pred_inter, T == 1 ? pred : nullptr,
+                    aff_bstride, off_bstride, B, H, W, 0, 0, 1, flags, gamma, aff_out, off_out,
+                    conf ? conf_out : nullptr, kind};
+    StepLaunch L1;
+    int rc = prepare_step(r1, L1);
+    if (rc) return rc;
     StepReq r{};
     r.dtype = dtype;
     r.kh = kh;
     r.kw = kw;
-    r.a = StepArgs{workspace, conf ? conf_out : nullptr, dep, aff_out, off_raw, pred_inter, pred,
-                   (long long)(K + 1) * HW, off_bstride, B, H, W, 0, 0, 1, flags};
+    r.a = StepArgs{pred_inter, conf ? conf_out : nullptr, dep, aff_out, off_raw, pred_inter, pred,
+                   (long long)(K + 1) * HW, off_bstride, B, H, W, 0, 0, 1, flags, nullptr, nullptr, nullptr, nullptr, 0};
     StepLaunch L;
-    int rc = prepare_step(r, L);
-    if (rc) return rc;
+    if (T > 1 && (rc = prepare_step(r, L))) return rc;
+    (void)workspace;
 
-    // prologue
-    const size_t vb = 4 * es;
-    const bool pvec = HW % 4 == 0 && aff_bstride % 4 == 0 && (!off_raw || off_bstride % 4 == 0) &&
-                      aligned(pred_init, vb) && aligned(dep, vb) && aligned(conf, vb) && aligned(aff_raw, vb) &&
-                      aligned(off_raw, vb) && aligned(aff_out, vb) && aligned(off_out, vb) && aligned(conf_out, vb) &&
-                      aligned(workspace, vb);
-    const void *pfn = dtype == NLSPN_DTYPE_F32 ? select_prologue<float>(K, pvec) : select_prologue<__half>(K, pvec);
-    if (!pfn) return fail(NLSPN_EUNSUPPORTED, "no prologue kernel for K=%d (supported 8, 16, 24, 48)", K);
-    PrologueArgs pa{pred_init, dep, conf, aff_raw, off_raw, gamma, aff_out, off_out, conf_out, workspace,
-                    aff_bstride, off_bstride, HW, B, kind, flags};
-    void *pargs[] = {&pa};
-    NLSPN_HIP_TRY(hipLaunchKernel(pfn, dim3(elementwise_grid(N)), dim3(256), pargs, 0, s));
-    if ((rc = check_launch("nlspn_propagate prologue"))) return rc;
-
-    // T fused iterations; list_pred[t] lands in pred_inter[t]
-    for (int t = 0; t < T; ++t) {
+    if ((rc = launch(L1, r1.a, s))) return rc;
+    for (int t = 1; t < T; ++t) {  // list_pred[t] lands in pred_inter[t]
         StepArgs a = r.a;
-        a.p_in = t == 0 ? workspace : static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
+        a.p_in = static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
         a.p_out = static_cast<char *>(pred_inter) + (size_t)t * N * es;
         a.pred_out = t == T - 1 ? pred : nullptr;
         if ((rc = launch(L, a, s))) return rc;
@@ -373,7 +362,7 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
     r.kh = kh;
     r.kw = kw;
     r.a = StepArgs{p_in, conf, dep, aff, off, p_out, nullptr, aff_bstride, off_bstride, B, H, W, 0, 0,
-                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags};
+                   off_layout == NLSPN_OFF_RAW ? 1 : 0, flags, nullptr, nullptr, nullptr, nullptr, 0};
     StepLaunch L;
     int rc = prepare_step(r, L);
     if (rc) return rc;

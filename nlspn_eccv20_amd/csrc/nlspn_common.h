@@ -156,6 +156,38 @@ template <> struct BVec<__half, 4> {
     }
 };
 
+enum { kAffAS = 0, kAffASS = 1, kAffTC = 2, kAffTGASS = 3 };
+
+// _affinity_normalization (nlspnmodel.py:179-201) on K raw taps in place, and the
+// reference-tap weight 1 - sum (_aff_insert :262-263) into `ref`; per pixel e.
+template <int K, int PX>
+__device__ __forceinline__ void normalize_taps(float (&t)[K][PX], float (&ref)[PX], int kind, float gamma) {
+#pragma unroll
+    for (int e = 0; e < PX; ++e) {
+        if (kind == kAffTC) {            // :182-183
+#pragma unroll
+            for (int k = 0; k < K; ++k) t[k][e] = tanhf(t[k][e]) / gamma;
+        } else if (kind == kAffTGASS) {  // :184-185
+            const float den = gamma + 1e-8f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) t[k][e] = tanhf(t[k][e]) / den;
+        }
+        float s = 0.f;                   // :190-191
+#pragma unroll
+        for (int k = 0; k < K; ++k) s += fabsf(t[k][e]);
+        s = s + 1e-4f;
+        if ((kind == kAffASS || kind == kAffTGASS) && s < 1.0f) s = 1.0f;  // :193-194
+        if (kind != kAffTC) {            // :196-197
+#pragma unroll
+            for (int k = 0; k < K; ++k) t[k][e] = t[k][e] / s;
+        }
+        float sum = 0.f;                 // :262-263
+#pragma unroll
+        for (int k = 0; k < K; ++k) sum += t[k][e];
+        ref[e] = 1.0f - sum;
+    }
+}
+
 // torch.clamp(x, min=0) (NaN propagates).
 __device__ __forceinline__ float clamp0(float v) { return v < 0.f ? 0.f : v; }
 

@@ -8,18 +8,26 @@
 //   preserve-input blend + optional clamp         (:355-361)   [+ final clamp :375-377 on the last]
 // with one launch, no `columns` buffer and no GEMM (the NLSPN weight is all ones).
 //
+// FIRST = the first iteration with the forward prologue fused in: it reads the
+// raw head outputs (pred_init, conf, raw affinity, raw offsets), builds p0 and
+// conf' on the fly (:328-348), normalises the affinity in-kernel
+// (_affinity_normalization + _aff_insert, :179-201, :261-269) and writes the
+// output-dict tensors (aff, confidence, inserted offsets) for its own pixels —
+// one pass instead of a separate prologue kernel plus a first step.
+//
 // Structure (one workgroup per TH x TW output tile, PX pixels per thread):
-//   1. issue the window's staging loads (p_in, conf; clamped, branch-free), then
-//      the tile's streamed loads — K normalised-affinity planes, 2K offset planes
-//      and dep — 16-B (fp32) / 8-B (fp16) per lane, coalesced;
-//   2. stage f = p_in * conf for the tile + halo window into LDS (fp32), zero
+//   1. issue the window's staging loads (p_in, conf [, dep]; clamped, branch-
+//      free), then the tile's streamed loads — K affinity planes, 2K offset
+//      planes and dep — coalesced, through wave-uniform buffer descriptors;
+//   2. stage f = p * conf for the tile + halo window into LDS (fp32), zero
 //      outside the image (= the reference's zero-padded bilinear) or replicate-
 //      clamped for the no-offset branch; an LDS-only barrier keeps the streamed
-//      loads in flight;
-//   3. per tap, bilinear-sample f from LDS; taps whose 2x2 footprint leaves the
-//      window (learned offsets are unbounded) are flagged and served afterwards
-//      from L2/global with the reference's per-corner checks — correctness never
-//      depends on the halo;
+//      loads in flight (s_waitcnt vmcnt counts in issue order, so staging waits
+//      only for its own loads and each tap only for the planes it consumes);
+//   3. pass A: per tap, bilinear-sample f from LDS; taps whose 2x2 footprint
+//      leaves the window (learned offsets are unbounded) are flagged; pass B
+//      (rare) serves them from L2/global with the reference's per-corner checks —
+//      correctness never depends on the halo;
 //   4. accumulate taps in index order with the reference tap (index K/2) weighted
 //      1 - sum(others); blend, clamp, store p_out (and pred on the last step).
 // Summation and bilinear arithmetic follow the reference's operation order; the
@@ -32,10 +40,10 @@
 namespace nlspn {
 
 struct StepArgs {
-    const void *p_in;   // B planes
-    const void *conf;   // B planes or null (conf_prop off)
+    const void *p_in;   // B planes (FIRST: pred_init)
+    const void *conf;   // B planes or null (conf_prop off). FIRST: raw confidence, else conf'
     const void *dep;    // B planes or null (preserve off)
-    const void *aff;    // normalised affinity, (K+1) planes per batch item
+    const void *aff;    // affinity: normalised (K+1) planes per item, or FIRST: raw K planes
     const void *off;    // offsets (null: no-offset branch)
     void *p_out;        // B planes
     void *pred_out;     // B planes or null
@@ -45,22 +53,41 @@ struct StepArgs {
     int tiles_x, tiles_y;
     int off_raw;        // 1: raw (2K planes, ref tap implicit), 0: inserted (2(K+1) planes)
     unsigned flags;     // NLSPN_PRESERVE_INPUT | NLSPN_ALWAYS_CLIP
+    // FIRST only
+    const float *gamma;  // device, 1 float (aff_scale_const)
+    void *aff_out;       // (K+1) planes per item, contiguous
+    void *off_out;       // 2(K+1) planes per item, contiguous, or null
+    void *conf_out;      // B planes, or null iff conf null
+    int kind;            // affinity kind
 };
 
 constexpr unsigned kPreserve = 0x1u;
 constexpr unsigned kAlwaysClip = 0x2u;
 
-// f = p * conf at pixel q of the batch item (buffer loads; conf may be absent)
-template <typename T>
-__device__ __forceinline__ float fetch_f(rsrc_t rp, rsrc_t rc, bool has_conf, unsigned q) {
-    float v[1];
-    BVec<T, 1>::load(rp, q * (unsigned)sizeof(T), 0u, v);
-    if (has_conf) {
-        float c[1];
-        BVec<T, 1>::load(rc, q * (unsigned)sizeof(T), 0u, c);
-        return v[0] * c[0];
+// Source value f at a pixel.  Steps t > 1: f = p * conf'.  FIRST: p0 =
+// (1-m)*pred_init + m*dep [clamped], conf' = (1-m)*conf + m, m = dep > 0
+// (nlspnmodel.py:328-348), f = p0 * conf'.
+template <bool FIRST>
+__device__ __forceinline__ float make_f(float p, float c, float d, bool has_conf, bool preserve, bool clip) {
+    if (FIRST) {
+        const float m = d > 0.f ? 1.f : 0.f;
+        if (preserve) {
+            p = (1.0f - m) * p + m * d;
+            c = (1.0f - m) * c + m;
+        }
+        if (clip) p = clamp0(p);
     }
-    return v[0];
+    return has_conf ? p * c : p;
+}
+
+template <typename T, bool FIRST>
+__device__ __forceinline__ float fetch_f(rsrc_t rp, rsrc_t rc, rsrc_t rd, bool has_conf, bool preserve, bool clip,
+                                         unsigned q) {
+    float v[1], c[1] = {1.f}, d[1] = {0.f};
+    BVec<T, 1>::load(rp, q, 0u, v);
+    if (has_conf) BVec<T, 1>::load(rc, q, 0u, c);
+    if (FIRST && preserve) BVec<T, 1>::load(rd, q, 0u, d);
+    return make_f<FIRST>(v[0], c[0], d[0], has_conf, preserve, clip);
 }
 
 // Workgroup barrier that orders LDS only (no global-memory release): it waits
@@ -74,14 +101,10 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // KH x KW taps; TH x TW tile; PX px per thread; window radii RY/RX; SV = staging
-// vector width (4 requires W % 4 == 0 and RX % 4 == 0); PRE = preload offsets
-// before the staging barrier.
-//
-// Load order matters (s_waitcnt vmcnt counts in issue order): the window's
-// staging loads go out FIRST with clamped, branch-free addresses, then the
-// streamed per-pixel planes; staging waits only for its own loads
-// (vmcnt(#streamed)), and each tap waits only for the planes it consumes.
-template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE>
+// vector width (4 requires W % 4 == 0 and RX % 4 == 0); PRE = issue every tap's
+// planes before the staging barrier (else inside pass A); FIRST = fused prologue.
+template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE,
+          bool FIRST>
 __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     constexpr int NT = TH * TW / PX;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
@@ -92,9 +115,11 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     static_assert(OFFSET || (KH == 3 && KW == 3 && RY == 1 && RX == 1), "no-offset branch is 3x3 replicate");
     static_assert(!OFFSET || (RY > PH && RX > PW), "window must cover the tap base grid");
     static_assert(SV == 1 || (OFFSET && RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
+    static_assert(!FIRST || PRE, "the fused prologue normalises all K taps up front");
     constexpr int WV = WW / SV;                  // staging vectors per window row
     constexpr int NV = WH * WV;                  // staging vectors per window
     constexpr int SIT = (NV + NT - 1) / NT;      // staging vectors per thread
+    constexpr unsigned ES = sizeof(T);
     __shared__ __attribute__((aligned(16))) float win[WH * WW];
 
     const int H = a.H, W = a.W;
@@ -107,22 +132,23 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     const int x0 = tx * TW, y0 = ty * TH;
     const int wy0 = y0 - RY, wx0 = x0 - RX;
 
-    constexpr unsigned ES = sizeof(T);
     const bool has_conf = a.conf != nullptr;
-    const rsrc_t rp = make_rsrc(static_cast<const T *>(a.p_in) + b * HW);
-    const rsrc_t rc = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : static_cast<const T *>(a.p_in));
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
+    const T *pbase = static_cast<const T *>(a.p_in) + b * HW;
+    const rsrc_t rp = make_rsrc(pbase);
+    const rsrc_t rc = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : pbase);
+    const rsrc_t rd = make_rsrc(preserve ? static_cast<const T *>(a.dep) + b * HW : pbase);
 
     const int ly = threadIdx.x / TPR, lx = (threadIdx.x % TPR) * PX;
     const int y = y0 + ly, xb = x0 + lx;
     const bool active = (y < H) && (xb < W);  // PX>1 requires W % PX == 0: groups are all-in or all-out
-    // Per-lane offsets are 32-bit (a plane holds < 2^31 pixels); plane bases are
-    // wave-uniform, so loads take the saddr + 32-bit voffset form (fewer VGPRs).
     const unsigned pix = active ? (unsigned)(y * W + xb) : 0u;  // inactive lanes load pixel 0 (in bounds)
+    const unsigned vpix = pix * ES;            // per-lane byte offset, shared by every plane
+    const unsigned plane_bytes = (unsigned)HW * ES;
 
-    // ---- 1. staging loads (first): f = p * conf over the window, clamped addresses
-    float sp[SIT][SV], sc[SIT][SV];
+    // ---- 1. staging loads (first): the window's p, conf [, dep], clamped addresses
+    float sp[SIT][SV], sc[SIT][SV], sd[FIRST ? SIT : 1][SV];
     bool sin[SIT];
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
@@ -130,32 +156,30 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
         const int ii = i < NV ? i : NV - 1;
         const int r = ii / WV, c = (ii - r * WV) * SV;
         int gy = wy0 + r, gx = wx0 + c;
-        if (OFFSET) {
-            sin[it] = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;   // zero padding outside
-        } else {
-            sin[it] = i < NV;                                              // replicate padding
-        }
+        if (OFFSET) sin[it] = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;  // zero padding outside
+        else sin[it] = i < NV;                                                   // replicate padding
         gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
         gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
         const unsigned q = (unsigned)(gy * W + gx) * ES;
         BVec<T, SV>::load(rp, q, 0u, sp[it]);
         if (has_conf) BVec<T, SV>::load(rc, q, 0u, sc[it]);
+        if (FIRST && preserve) BVec<T, SV>::load(rd, q, 0u, sd[FIRST ? it : 0]);
     }
 
-    // ---- 2. streamed per-pixel loads: K affinity planes, 2K offset planes, dep.
-    // PRE (small K): all issued now, before the staging barrier; otherwise each
-    // tap's planes are loaded inside pass A below.
+    // ---- 2. streamed per-pixel loads: K affinity planes, 2K offset planes, dep [, conf].
     float av[PRE ? K : 1][PX];
     float dh[PRE ? K : 1][PX], dw[PRE ? K : 1][PX];
-    float dv[PX];
+    float dv[PX], cv[PX];
+#pragma unroll
+    for (int p = 0; p < PX; ++p) dv[p] = cv[p] = 0.f;
     const rsrc_t ra = make_rsrc(static_cast<const T *>(a.aff) + b * a.aff_bs);
     const rsrc_t ro = make_rsrc(OFFSET ? static_cast<const T *>(a.off) + b * a.off_bs : static_cast<const T *>(a.aff));
-    const unsigned vpix = pix * ES;            // per-lane byte offset, shared by every plane
-    const unsigned plane_bytes = (unsigned)HW * ES;
     if (PRE) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            BVec<T, PX>::load(ra, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, av[PRE ? k : 0]);
+            // FIRST: raw affinity (K planes); otherwise the normalised (K+1)-plane layout
+            const unsigned ap = FIRST ? (unsigned)k : (unsigned)(k < REF ? k : k + 1);
+            BVec<T, PX>::load(ra, vpix, ap * plane_bytes, av[PRE ? k : 0]);
             if (OFFSET) {
                 const unsigned c = a.off_raw ? k : (k < REF ? k : k + 1);
                 BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, dh[PRE ? k : 0]);
@@ -163,7 +187,8 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
             }
         }
     }
-    if (preserve) BVec<T, PX>::load(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
+    if (preserve) BVec<T, PX>::load(rd, vpix, 0u, dv);
+    if (FIRST && has_conf) BVec<T, PX>::load(rc, vpix, 0u, cv);
 
     // ---- 3. finish staging into LDS (waits for the staging loads only)
 #pragma unroll
@@ -173,7 +198,8 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
             float v[SV];
 #pragma unroll
             for (int e = 0; e < SV; ++e) {
-                const float f = has_conf ? sp[it][e] * sc[it][e] : sp[it][e];
+                const float f = make_f<FIRST>(sp[it][e], has_conf ? sc[it][e] : 1.f,
+                                              FIRST && preserve ? sd[FIRST ? it : 0][e] : 0.f, has_conf, preserve, clip);
                 v[e] = sin[it] ? f : 0.f;
             }
             const int r = i / WV, c = (i - r * WV) * SV;
@@ -186,12 +212,43 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     lds_barrier();
     if (!active) return;  // no barrier below
 
+    // ---- FIRST: the prologue's per-pixel outputs (normalised affinity, conf', offsets)
+    float fref_a[PX];  // FIRST: reference-tap weight from the normalisation (== 1 - sum, same order)
+    if (FIRST) {
+        normalize_taps<K, PX>(av, fref_a, a.kind, *a.gamma);
+        const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + b * (K + 1) * HW);
+#pragma unroll
+        for (int c = 0; c < K + 1; ++c)
+            BVec<T, PX>::store(rao, vpix, (unsigned)c * plane_bytes, c == REF ? fref_a : av[c < REF ? c : c - 1]);
+        if (has_conf) {
+            float co[PX];
+#pragma unroll
+            for (int p = 0; p < PX; ++p) {
+                const float m = dv[p] > 0.f ? 1.f : 0.f;
+                co[p] = preserve ? (1.0f - m) * cv[p] + m : cv[p];
+            }
+            BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.conf_out) + b * HW), vpix, 0u, co);
+        }
+        if (OFFSET && a.off_out) {
+            const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + b * 2 * (K + 1) * HW);
+            float z[PX];
+#pragma unroll
+            for (int p = 0; p < PX; ++p) z[p] = 0.f;
+#pragma unroll
+            for (int c = 0; c < K + 1; ++c) {
+                const int k = c < REF ? c : c - 1;
+                BVec<T, PX>::store(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : dh[PRE ? k : 0]);
+                BVec<T, PX>::store(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : dw[PRE ? k : 0]);
+            }
+        }
+    }
+
     // ---- 4. taps.  Pass A (LDS only, no divergent global loads, so the
     // compiler's vmcnt waits stay counted per tap): col[k] = bilinear * a_k for
     // every tap whose 2x2 footprint is inside the window; out-of-window taps are
     // flagged in `fb`.  Pass B (rare): flagged taps from L2/global with the
-    // reference's per-corner checks (their offsets/affinity re-read from cache).
-    // Then accumulate in tap index order with the reference tap (K/2) weighted
+    // reference's per-corner checks (their offsets re-read from cache).  Then
+    // accumulate in tap index order with the reference tap (K/2) weighted
     // 1 - sum(others) (nlspnmodel.py:262-263): the reference's summation order,
     // whichever pass served a tap.  col = val * a then acc += col is the same
     // IEEE sequence as acc += val * a (no contraction).
@@ -267,16 +324,21 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
                 const float h_im = (float)(y - PH + i) + o1[0];
                 BVec<T, 1>::load(ro, vpix + p * ES, (2 * c + 1) * plane_bytes, o1);
                 const float w_im = (float)(xb + p - PW + j) + o1[0];
-                BVec<T, 1>::load(ra, vpix + p * ES, (unsigned)t * plane_bytes, a1);
+                if (FIRST) a1[0] = av[PRE ? k : 0][p];  // normalised in registers above
+                else BVec<T, 1>::load(ra, vpix + p * ES, (unsigned)t * plane_bytes, a1);
                 const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
                 const int h_high = h_low + 1, w_high = w_low + 1;
                 const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
                 const float hh = 1.f - lh, hw = 1.f - lw;
                 const int r0 = h_low * W, r1 = h_high * W;
-                const float v1 = (h_low >= 0 && w_low >= 0) ? fetch_f<T>(rp, rc, has_conf, r0 + w_low) : 0.f;
-                const float v2 = (h_low >= 0 && w_high <= W - 1) ? fetch_f<T>(rp, rc, has_conf, r0 + w_high) : 0.f;
-                const float v3 = (h_high <= H - 1 && w_low >= 0) ? fetch_f<T>(rp, rc, has_conf, r1 + w_low) : 0.f;
-                const float v4 = (h_high <= H - 1 && w_high <= W - 1) ? fetch_f<T>(rp, rc, has_conf, r1 + w_high) : 0.f;
+                const float v1 = (h_low >= 0 && w_low >= 0)
+                                     ? fetch_f<T, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + w_low) * ES) : 0.f;
+                const float v2 = (h_low >= 0 && w_high <= W - 1)
+                                     ? fetch_f<T, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + w_high) * ES) : 0.f;
+                const float v3 = (h_high <= H - 1 && w_low >= 0)
+                                     ? fetch_f<T, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + w_low) * ES) : 0.f;
+                const float v4 = (h_high <= H - 1 && w_high <= W - 1)
+                                     ? fetch_f<T, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + w_high) * ES) : 0.f;
                 const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
                 col[k][p] = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4) * a1[0];
             }
@@ -286,7 +348,8 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
         // reference tap: zero offset, integer sample point -> bilinear weight exactly (1,0,0,0)
-        const float cref = win[(ly + RY) * WW + lx + p + RX] * (1.0f - asum[p]);
+        const float aref = FIRST ? fref_a[p] : 1.0f - asum[p];
+        const float cref = win[(ly + RY) * WW + lx + p + RX] * aref;
         acc[p] = 0.f;
 #pragma unroll
         for (int t = 0; t < KK; ++t) acc[p] += t == REF ? cref : col[t < REF ? t : t - 1][p];

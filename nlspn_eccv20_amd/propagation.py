@@ -167,7 +167,7 @@ def _alloc_outputs(pred_init, K, T, with_off, with_conf):
         "aff": torch.empty((B, K + 1, H, W), **kw_),
         "offset": torch.empty((B, 2 * (K + 1), H, W), **kw_) if with_off else None,
         "confidence": torch.empty((B, 1, H, W), **kw_) if with_conf else None,
-        "workspace": torch.empty((B, 1, H, W), **kw_),
+        "workspace": None,  # the prologue is fused into the first iteration (no scratch plane)
     }
 
 

@@ -17,7 +17,6 @@
 #include <string>
 #include <vector>
 
-#include "../nlspn_eccv20_amd/csrc/nlspn_prologue.h"
 #include "../nlspn_eccv20_amd/csrc/nlspn_step.h"
 
 using namespace nlspn;
@@ -39,7 +38,7 @@ struct Variant {
 
 template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool PRE>
 Variant mk(const char *name) {
-    return Variant{name, reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, true, PRE>),
+    return Variant{name, reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, true, PRE, false>),
                    TH, TW, PX};
 }
 
@@ -71,6 +70,35 @@ __global__ void __launch_bounds__(256) stream_ceiling(StepArgs a) {
     Vec<float, PX>::load(static_cast<const float *>(a.conf) + b * HW + q, v);
     for (int e = 0; e < PX; ++e) acc[e] += v[e];
     Vec<float, PX>::store(static_cast<float *>(a.p_out) + b * HW + q, acc);
+}
+
+// Generic memory-only ceiling over the step kernel's exact plane set (K aff, 2K
+// offsets, dep, p_in, conf; one plane written), PX pixels per lane, buffer loads.
+template <typename T, int K, int PX>
+__global__ void __launch_bounds__(256) stream_ceiling_t(StepArgs a) {
+    const unsigned HW = (unsigned)a.H * a.W, ES = sizeof(T);
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (g * PX >= (long long)a.B * HW) return;
+    const unsigned b = (unsigned)((g * PX) / HW), q = (unsigned)((g * PX) % HW);
+    const rsrc_t ra = make_rsrc(static_cast<const T *>(a.aff) + b * a.aff_bs);
+    const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + b * a.off_bs);
+    float acc[PX] = {0}, v[PX];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        BVec<T, PX>::load(ra, q * ES, (k < K / 2 ? k : k + 1) * HW * ES, v);
+        for (int e = 0; e < PX; ++e) acc[e] += v[e];
+        BVec<T, PX>::load(ro, q * ES, 2 * k * HW * ES, v);
+        for (int e = 0; e < PX; ++e) acc[e] += v[e];
+        BVec<T, PX>::load(ro, q * ES, (2 * k + 1) * HW * ES, v);
+        for (int e = 0; e < PX; ++e) acc[e] += v[e];
+    }
+    BVec<T, PX>::load(make_rsrc(static_cast<const T *>(a.dep) + b * HW), q * ES, 0, v);
+    for (int e = 0; e < PX; ++e) acc[e] += v[e];
+    BVec<T, PX>::load(make_rsrc(static_cast<const T *>(a.p_in) + b * HW), q * ES, 0, v);
+    for (int e = 0; e < PX; ++e) acc[e] += v[e];
+    BVec<T, PX>::load(make_rsrc(static_cast<const T *>(a.conf) + b * HW), q * ES, 0, v);
+    for (int e = 0; e < PX; ++e) acc[e] += v[e];
+    BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.p_out) + b * HW), q * ES, 0, acc);
 }
 
 template <typename T> std::vector<T> conv(const std::vector<float> &v);
@@ -105,7 +133,12 @@ template <> std::vector<Variant> variants<__half, 1, 17>() {
         mk<__half, 1, 17, 4, 32, 1, 8, 16, 4, true>("4x32 px1 (128t)"),
         mk<__half, 1, 17, 8, 32, 1, 8, 16, 4, false>("8x32 px1 nopre"),
         mk<__half, 1, 17, 8, 32, 1, 4, 12, 4, true>("8x32 px1 RY4 RX12"),
-        mk<__half, 1, 17, 16, 64, 4, 8, 16, 4, true>("16x64 px4"),
+        mk<__half, 1, 17, 8, 64, 2, 8, 16, 4, true>("8x64 px2"),
+        mk<__half, 1, 17, 4, 64, 2, 8, 16, 4, true>("4x64 px2 (128t)"),
+        mk<__half, 1, 17, 16, 32, 2, 8, 16, 4, true>("16x32 px2"),
+        mk<__half, 1, 17, 8, 32, 2, 8, 16, 4, true>("8x32 px2 (128t)"),
+        mk<__half, 1, 17, 8, 64, 2, 8, 16, 4, false>("8x64 px2 nopre"),
+        mk<__half, 1, 17, 4, 64, 4, 8, 16, 4, true>("4x64 px4 (64t)"),
     };
 }
 
@@ -254,12 +287,12 @@ int run(int B, int H, int W, int reps, int rounds, float sigma) {
         printf("%-26s %10.2f %10.2f %10.0f\n", vs[vi].name.c_str(), med * 1e3, mn * 1e3, bytes / (med * 1e-3) / 1e9);
     }
 
-    for (int px : {1, 4}) {
-        if (ES != 4 || K != 8) break;
+    for (int px : {1, 2, 4}) {
         StepArgs a = args_for(vs[0]);
         void *kargs[] = {&a};
-        const void *fn = px == 1 ? reinterpret_cast<const void *>(&stream_ceiling<1>)
-                                 : reinterpret_cast<const void *>(&stream_ceiling<4>);
+        const void *fn = px == 1 ? reinterpret_cast<const void *>(&stream_ceiling_t<T, K, 1>)
+                       : px == 2 ? reinterpret_cast<const void *>(&stream_ceiling_t<T, K, 2>)
+                                 : reinterpret_cast<const void *>(&stream_ceiling_t<T, K, 4>);
         unsigned grid = (unsigned)((N / px + 255) / 256);
         std::vector<float> ts;
         for (int r = 0; r < rounds; ++r) {
@@ -275,33 +308,6 @@ int run(int B, int H, int W, int reps, int rounds, float sigma) {
                bytes / (ts[ts.size() / 2] * 1e-3) / 1e9);
     }
 
-    // ---- prologue variants (K=8): write aff_out, off_out, conf_out, p0
-    struct PV { const char *name; const void *fn; int px; };
-    std::vector<PV> pv = {{"prologue px1", reinterpret_cast<const void *>(&prologue_kernel<T, K, 1>), 1},
-                          {"prologue px2", reinterpret_cast<const void *>(&prologue_kernel<T, K, 2>), 2}};
-    float *gam;
-    CK(hipMalloc(&gam, 4));
-    float g4 = 0.5f * K;
-    CK(hipMemcpy(gam, &g4, 4, hipMemcpyHostToDevice));
-    T *ao = dscratch, *oo = dscratch + (size_t)B * (K + 1) * HW, *co = oo + (size_t)B * 2 * (K + 1) * HW, *p0 = co + N;
-    for (auto &v : pv) {
-        PrologueArgs pa{dp, dd, dc, dr, doff, gam, ao, oo, co, p0, (long long)K * HW, (long long)2 * K * HW, HW, B, 3, 1u};
-        void *kargs[] = {&pa};
-        long long groups = N / v.px;
-        unsigned grid = (unsigned)std::min<long long>((groups + 255) / 256, 4096);
-        std::vector<float> ts;
-        for (int r = 0; r < rounds; ++r) {
-            for (int i = 0; i < reps; ++i)
-                CK(hipExtLaunchKernel(v.fn, dim3(grid), dim3(256), kargs, 0, s, ev[2 * i], ev[2 * i + 1], 0));
-            CK(hipStreamSynchronize(s));
-            double sum = 0;
-            for (int i = 0; i < reps; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1])); sum += ms; }
-            ts.push_back((float)(sum / reps));
-        }
-        std::sort(ts.begin(), ts.end());
-        const double pb = (double)ES * (3 * K + 3 + 3 * (K + 1) + 2);
-        printf("%-26s %10.2f us  (%.0f GB/s of %.0f B/px)\n", v.name, ts[ts.size() / 2] * 1e3, pb * N / (ts[ts.size() / 2] * 1e-3) / 1e9, pb);
-    }
     return 0;
 }
 
