@@ -236,3 +236,211 @@ int FN(orc_propagate)(const REAL *pred_init, const REAL *dep, const REAL *conf,
     if (cf && cf != conf_out) free(cf);
     return 0;
 }
+
+/* ------------------------------------------------------------------ backward
+ * Gradient of the propagation section (autograd of nlspnmodel.py:323-381 with the
+ * DCN backward of modulated_deform_conv_cuda.cu:124-280):
+ *   grad_mask  (col2im_coord mval, .cuh:304-307): sum col * bilinear(im, h, w)
+ *   grad_offset(col2im_coord val,  .cuh:309-312): sum coordinate_weight * col * mask,
+ *              coordinate weight mdmcn_get_coordinate_weight (.cuh:84-125)
+ *   grad_input (col2im, .cuh:196-254): bilinear weight (mdmcn_get_gradient_weight,
+ *              .cuh:57-81) * col * mask scattered to the 4 corners
+ * with col = grad_output (NLSPN weight = 1).  The elementwise parts follow torch's
+ * autograd: clamp(min=0) passes grad where x >= 0; abs -> sign; masked s[s<1]=1
+ * blocks the gradient; tanh -> 1 - y^2.  Gradients of dep are not produced.
+ * grad_inter (T x N) may be NULL; grad_off_raw/grad_conf/grad_gamma may be NULL. */
+static REAL FN(orc_coord_weight)(REAL h, REAL w, int H, int W, const REAL *im, int dir)
+{
+    if (h <= -1 || h >= H || w <= -1 || w >= W) return 0;  /* .cuh:88-92 */
+    int h_low = (int)FLOOR(h), w_low = (int)FLOOR(w);
+    int h_high = h_low + 1, w_high = w_low + 1;
+    REAL weight = 0;
+    if (dir == 0) {
+        if (h_low >= 0 && w_low >= 0) weight += -1 * (w_low + 1 - w) * im[(long long)h_low * W + w_low];
+        if (h_low >= 0 && w_high <= W - 1) weight += -1 * (w - w_low) * im[(long long)h_low * W + w_high];
+        if (h_high <= H - 1 && w_low >= 0) weight += (w_low + 1 - w) * im[(long long)h_high * W + w_low];
+        if (h_high <= H - 1 && w_high <= W - 1) weight += (w - w_low) * im[(long long)h_high * W + w_high];
+    } else {
+        if (h_low >= 0 && w_low >= 0) weight += -1 * (h_low + 1 - h) * im[(long long)h_low * W + w_low];
+        if (h_low >= 0 && w_high <= W - 1) weight += (h_low + 1 - h) * im[(long long)h_low * W + w_high];
+        if (h_high <= H - 1 && w_low >= 0) weight += -1 * (h - h_low) * im[(long long)h_high * W + w_low];
+        if (h_high <= H - 1 && w_high <= W - 1) weight += (h - h_low) * im[(long long)h_high * W + w_high];
+    }
+    return weight;
+}
+
+int FN(orc_propagate_backward)(const REAL *pred_init, const REAL *dep, const REAL *conf,
+                               const REAL *aff_raw, long long aff_bstride,
+                               const REAL *off_raw, long long off_bstride,
+                               REAL gamma, int kind, int kh, int kw, int T, unsigned flags,
+                               int B, int H, int W,
+                               const REAL *grad_pred, const REAL *grad_inter,
+                               REAL *grad_pred_init, REAL *grad_conf, REAL *grad_aff_raw,
+                               REAL *grad_off_raw, REAL *grad_gamma)
+{
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    const int K = kh * kw - 1, KK = K + 1, REF = K / 2;
+    const int ph = (kh - 1) / 2, pw = (kw - 1) / 2;
+    const int preserve = (flags & ORC_PRESERVE) != 0;
+    const int clip = (flags & ORC_ALWAYS_CLIP) != 0;
+    if (K < 1 || K > 63 || (kh % 2) == 0 || (kw % 2) == 0 || T < 1) return 1;
+    if (off_raw == NULL && K != 8) return 2;
+
+    /* forward recompute, keeping p_0..p_T and the pre-clamp values */
+    REAL *aff = (REAL *)malloc(sizeof(REAL) * KK * N);
+    REAL *offi = off_raw ? (REAL *)malloc(sizeof(REAL) * 2 * KK * N) : NULL;
+    REAL *cf = (REAL *)malloc(sizeof(REAL) * N);
+    REAL *m = (REAL *)malloc(sizeof(REAL) * N);
+    REAL *p = (REAL *)malloc(sizeof(REAL) * (T + 1) * N);
+    REAL *pre = (REAL *)malloc(sizeof(REAL) * (T + 1) * N);
+    REAL *f = (REAL *)malloc(sizeof(REAL) * N);
+    FN(orc_aff_norm)(aff_raw, aff_bstride, B, K, HW, kind, gamma, aff);
+    if (offi) FN(orc_off_insert)(off_raw, off_bstride, B, K, HW, offi);
+    for (long long i = 0; i < N; ++i) {
+        m[i] = preserve ? (dep[i] > 0 ? (REAL)1 : (REAL)0) : (REAL)0;
+        REAL c = conf ? conf[i] : (REAL)1;
+        if (conf && preserve) c = ((REAL)1.0 - m[i]) * c + m[i];
+        cf[i] = c;
+        REAL v = pred_init[i];
+        if (preserve) v = ((REAL)1.0 - m[i]) * v + m[i] * dep[i];
+        pre[i] = v;
+        p[i] = clip ? FN(orc_clamp0)(v) : v;
+    }
+    for (int t = 1; t <= T; ++t) {
+        const REAL *pp = p + (long long)(t - 1) * N;
+        for (long long i = 0; i < N; ++i) f[i] = conf ? pp[i] * cf[i] : pp[i];
+        REAL *o = p + (long long)t * N, *pr = pre + (long long)t * N;
+        if (offi) FN(orc_mdcn_c1)(f, offi, aff, B, H, W, kh, kw, ph, pw, o);
+        else FN(orc_prop_noffset)(f, aff, B, H, W, o);
+        for (long long i = 0; i < N; ++i) {
+            REAL v = o[i];
+            if (preserve) v = ((REAL)1.0 - m[i]) * v + m[i] * dep[i];
+            pr[i] = v;
+            o[i] = clip ? FN(orc_clamp0)(v) : v;
+        }
+    }
+
+    /* reverse sweep */
+    REAL *gaff = (REAL *)calloc((size_t)KK * N, sizeof(REAL));
+    REAL *goff = (REAL *)calloc((size_t)2 * KK * N, sizeof(REAL));
+    REAL *gcf = (REAL *)calloc((size_t)N, sizeof(REAL));
+    REAL *gp = (REAL *)calloc((size_t)N, sizeof(REAL)); /* dL/dp_t */
+    REAL *gf = (REAL *)calloc((size_t)N, sizeof(REAL)); /* dL/df_{t-1} */
+    for (long long i = 0; i < N; ++i) {
+        REAL g = grad_inter ? grad_inter[(long long)(T - 1) * N + i] : 0;
+        if (grad_pred) g += clip ? grad_pred[i] : (p[(long long)T * N + i] >= 0 ? grad_pred[i] : 0);
+        gp[i] = g;
+    }
+    for (int t = T; t >= 1; --t) {
+        const REAL *pp = p + (long long)(t - 1) * N, *pr = pre + (long long)t * N;
+        for (long long i = 0; i < N; ++i) f[i] = conf ? pp[i] * cf[i] : pp[i];
+        for (long long i = 0; i < N; ++i) gf[i] = 0;
+        for (int b = 0; b < B; ++b)
+            for (int y = 0; y < H; ++y)
+                for (int x = 0; x < W; ++x) {
+                    const long long q = (long long)y * W + x, i = b * HW + q;
+                    REAL g = gp[i];
+                    if (clip && !(pr[i] >= 0)) g = 0;
+                    const REAL go = preserve ? ((REAL)1.0 - m[i]) * g : g;
+                    const REAL *fb = f + b * HW;
+                    REAL *gfb = gf + b * HW;
+                    for (int tap = 0; tap < KK; ++tap) {
+                        const int ii = tap / kw, jj = tap % kw;
+                        const REAL a = aff[((long long)b * KK + tap) * HW + q];
+                        REAL hs, ws;
+                        if (offi) {
+                            hs = (y - ph + ii) + offi[((long long)b * 2 * KK + 2 * tap) * HW + q];
+                            ws = (x - pw + jj) + offi[((long long)b * 2 * KK + 2 * tap + 1) * HW + q];
+                        } else { /* replicate padding: clamp the integer sample point */
+                            int yy = y + ii - 1, xx = x + jj - 1;
+                            yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+                            xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+                            hs = yy; ws = xx;
+                        }
+                        if (!(hs > -1 && ws > -1 && hs < H && ws < W)) continue;
+                        const REAL val = FN(orc_bilinear)(fb, H, W, hs, ws);
+                        gaff[((long long)b * KK + tap) * HW + q] += go * val;           /* mval */
+                        if (offi) {
+                            goff[((long long)b * 2 * KK + 2 * tap) * HW + q] +=
+                                FN(orc_coord_weight)(hs, ws, H, W, fb, 0) * go * a;     /* .cuh:309 */
+                            goff[((long long)b * 2 * KK + 2 * tap + 1) * HW + q] +=
+                                FN(orc_coord_weight)(hs, ws, H, W, fb, 1) * go * a;
+                        }
+                        const REAL top = go * a;                                          /* .cuh:236 */
+                        const int hl = (int)FLOOR(hs), wl = (int)FLOOR(ws);
+                        const REAL lh = hs - hl, lw = ws - wl, hh = 1 - lh, hw = 1 - lw;
+                        if (hl >= 0 && wl >= 0) gfb[(long long)hl * W + wl] += hh * hw * top;
+                        if (hl >= 0 && wl + 1 <= W - 1) gfb[(long long)hl * W + wl + 1] += hh * lw * top;
+                        if (hl + 1 <= H - 1 && wl >= 0) gfb[(long long)(hl + 1) * W + wl] += lh * hw * top;
+                        if (hl + 1 <= H - 1 && wl + 1 <= W - 1) gfb[(long long)(hl + 1) * W + wl + 1] += lh * lw * top;
+                    }
+                }
+        /* f_{t-1} = p_{t-1} * conf' ; p_{t-1} = clamp(blend(...)) */
+        for (long long i = 0; i < N; ++i) {
+            if (conf) gcf[i] += gf[i] * pp[i];
+            REAL g = conf ? gf[i] * cf[i] : gf[i];
+            if (t - 1 >= 1 && grad_inter) g += grad_inter[(long long)(t - 2) * N + i];
+            gp[i] = g;
+        }
+    }
+    /* p_0 = clamp(blend(pred_init)) */
+    for (long long i = 0; i < N; ++i) {
+        REAL g = gp[i];
+        if (clip && !(pre[i] >= 0)) g = 0;
+        grad_pred_init[i] = preserve ? ((REAL)1.0 - m[i]) * g : g;
+        if (grad_conf) grad_conf[i] = conf ? (preserve ? ((REAL)1.0 - m[i]) * gcf[i] : gcf[i]) : 0;
+    }
+    /* _off_insert backward: drop the reference pair */
+    if (grad_off_raw && offi)
+        for (int b = 0; b < B; ++b)
+            for (int k = 0; k < K; ++k) {
+                const int tap = k < REF ? k : k + 1;
+                for (long long q = 0; q < 2 * HW; ++q)
+                    grad_off_raw[((long long)b * 2 * K + 2 * k) * HW + q] = goff[((long long)b * 2 * KK + 2 * tap) * HW + q];
+            }
+    /* _aff_insert + _affinity_normalization backward */
+    REAL gg = 0;
+    for (int b = 0; b < B; ++b)
+        for (long long q = 0; q < HW; ++q) {
+            REAL u[64], G[64], th[64];
+            const REAL gref = gaff[((long long)b * KK + REF) * HW + q];
+            REAL s = 0;
+            for (int k = 0; k < K; ++k) {
+                const int tap = k < REF ? k : k + 1;
+                G[k] = gaff[((long long)b * KK + tap) * HW + q] - gref;          /* aff_ref = 1 - sum */
+                const REAL a = aff_raw[b * aff_bstride + k * HW + q];
+                th[k] = TANH(a);
+                u[k] = kind == ORC_TC ? th[k] / gamma : (kind == ORC_TGASS ? th[k] / (gamma + (REAL)1e-8) : a);
+                s += FABS(u[k]);
+            }
+            s = s + (REAL)1e-4;
+            const int clamped = (kind == ORC_ASS || kind == ORC_TGASS) && s < (REAL)1.0;
+            const REAL se = clamped ? (REAL)1.0 : s;
+            REAL dot = 0;
+            for (int k = 0; k < K; ++k) dot += G[k] * u[k];
+            for (int k = 0; k < K; ++k) {
+                REAL gu;
+                if (kind == ORC_TC) gu = G[k];
+                else {
+                    gu = G[k] / se;
+                    if (!clamped) {
+                        const REAL sg = u[k] > 0 ? (REAL)1 : (u[k] < 0 ? (REAL)-1 : (REAL)0);
+                        gu += -dot / (se * se) * sg;
+                    }
+                }
+                REAL ga = gu;
+                if (kind == ORC_TC) ga = gu * (1 - th[k] * th[k]) / gamma;
+                else if (kind == ORC_TGASS) {
+                    const REAL d = gamma + (REAL)1e-8;
+                    ga = gu * (1 - th[k] * th[k]) / d;
+                    gg += -gu * th[k] / (d * d);
+                }
+                grad_aff_raw[((long long)b * K + k) * HW + q] = ga;
+            }
+        }
+    if (grad_gamma) *grad_gamma = kind == ORC_TGASS ? gg : 0;
+
+    free(aff); free(offi); free(cf); free(m); free(p); free(pre); free(f);
+    free(gaff); free(goff); free(gcf); free(gp); free(gf);
+    return 0;
+}

@@ -146,3 +146,31 @@ def propagate(pred_init, dep, conf, aff_raw, off_raw, gamma, *, kind="TGASS", kh
         raise ValueError(f"oracle propagate rejected its arguments (code {rc})")
     return {"pred": pred, "pred_inter": pred_inter, "aff": aff_out,
             "offset": off_out, "confidence": conf_out}
+
+
+def propagate_backward(pred_init, dep, conf, aff_raw, off_raw, gamma, grad_pred, grad_inter=None, *,
+                       kind="TGASS", kh=3, kw=3, prop_time=18, preserve_input=True, always_clip=False):
+    """Gradient of propagate() (autograd of nlspnmodel.py:323-381 through the DCN backward,
+    modulated_deform_conv_cuda.cu:124-280).  Returns dict of grads: pred_init, confidence,
+    aff (raw, B,K,H,W), offset (raw, B,2K,H,W) or None, gamma (float)."""
+    dtype = pred_init.dtype
+    sfx, cr = _sfx(dtype)
+    pred_init, dep, conf, aff_raw, off_raw, grad_pred, grad_inter = (
+        _c(x, dtype) for x in (pred_init, dep, conf, aff_raw, off_raw, grad_pred, grad_inter))
+    B, _, H, W = pred_init.shape
+    K = kh * kw - 1
+    flags = (PRESERVE if preserve_input else 0) | (ALWAYS_CLIP if always_clip else 0)
+    g_pi = np.empty((B, 1, H, W), dtype=dtype)
+    g_conf = np.zeros((B, 1, H, W), dtype=dtype)
+    g_aff = np.empty((B, K, H, W), dtype=dtype)
+    g_off = None if off_raw is None else np.empty((B, 2 * K, H, W), dtype=dtype)
+    g_gamma = np.zeros(1, dtype=dtype)
+    fn = getattr(lib(), f"orc_propagate_backward_{sfx}")
+    fn.restype = ctypes.c_int
+    rc = fn(_p(pred_init), _p(dep), _p(conf), _p(aff_raw), ctypes.c_longlong(K * H * W),
+            _p(off_raw), ctypes.c_longlong(2 * K * H * W), cr(gamma), AFFINITY_KINDS[kind], kh, kw, prop_time,
+            flags, B, H, W, _p(grad_pred), _p(grad_inter), _p(g_pi), _p(g_conf), _p(g_aff), _p(g_off), _p(g_gamma))
+    if rc != 0:
+        raise ValueError(f"oracle backward rejected its arguments (code {rc})")
+    return {"pred_init": g_pi, "confidence": g_conf if conf is not None else None, "aff": g_aff,
+            "offset": g_off, "gamma": float(g_gamma[0])}
