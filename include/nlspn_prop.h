@@ -139,6 +139,31 @@ int nlspn_plan_launch(nlspn_plan_t plan, void *stream);
 int nlspn_plan_destroy(nlspn_plan_t plan);
 
 /*
+ * Backward of nlspn_propagate (float32 storage): what autograd computes through
+ * src/model/nlspnmodel.py:323-381 with the DCNv2 backward for each of the T DCN
+ * calls (modulated_deform_conv_cuda.cu:124-280; vision.cpp:10 ->
+ * modulated_deform_conv.h:46-86).  Takes the forward's inputs and its saved
+ * outputs (pred_inter, aff_out as aff_norm, conf_out as conf_eff) and the
+ * incoming gradients (grad_pred and/or grad_pred_inter, T x B planes; either may
+ * be NULL).  Writes grad_pred_init (B planes), grad_conf (B planes, iff conf),
+ * grad_aff_raw (B x K planes, contiguous), grad_off_raw (B x 2K planes,
+ * contiguous, iff off_raw), grad_gamma (1 float, TGASS only; may be NULL).
+ * dep receives no gradient (the reference's sparse input).  workspace:
+ * nlspn_backward_workspace_bytes() bytes.  dL/df is scattered with float
+ * atomics (as the reference's col2im), so its last bits depend on arrival order.
+ */
+size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw);
+int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
+                             const void *aff_raw, int64_t aff_bstride,
+                             const void *off_raw, int64_t off_bstride, const float *gamma,
+                             const void *pred_inter, const void *aff_norm, const void *conf_eff,
+                             const void *grad_pred, const void *grad_pred_inter,
+                             void *grad_pred_init, void *grad_conf, void *grad_aff_raw,
+                             void *grad_off_raw, float *grad_gamma, void *workspace,
+                             int B, int H, int W, int kh, int kw, int T, int kind,
+                             unsigned flags, void *stream);
+
+/*
  * Modulated DCNv2 forward, seam 2 of the drop-in (the `DCN` pybind module,
  * src/model/deformconv/src/vision.cpp:9, modulated_deform_conv.h:10-44,
  * cuda/modulated_deform_conv_cuda.cu:19-121), as one direct (GEMM-free) gather

@@ -13,6 +13,7 @@
 #include "../../include/nlspn_prop.h"
 #include "nlspn_mdcn.h"
 #include "nlspn_affnorm.h"
+#include "nlspn_backward.h"
 #include "nlspn_step.h"
 
 using namespace nlspn;
@@ -157,6 +158,55 @@ const void *select_affnorm(int K, bool vec) {
         case 16: return affnorm_fn<T, 16>(vec);
         case 24: return affnorm_fn<T, 24>(vec);
         case 48: return affnorm_fn<T, 48>(vec);
+        default: return nullptr;
+    }
+}
+
+// ---------------------------------------------------------------- backward dispatch
+struct BwdLaunch {
+    const void *fn = nullptr;
+    dim3 grid, block;
+};
+
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET>
+BwdLaunch make_bwd(BwdArgs &a, bool first) {
+    BwdLaunch L;
+    L.fn = first ? reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, true>)
+                 : reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, false>);
+    a.tiles_x = (a.W + TW - 1) / TW;
+    a.tiles_y = (a.H + TH - 1) / TH;
+    L.grid = dim3((unsigned)(a.B * a.tiles_x * a.tiles_y));
+    L.block = dim3(TH * TW);
+    return L;
+}
+
+int select_bwd(BwdArgs &a, int kh, int kw, bool offset, bool vec, bool first, BwdLaunch &L) {
+    if (!offset) {
+        if (kh != 3 || kw != 3)
+            return fail(NLSPN_EUNSUPPORTED, "no-offset propagation is 3x3 replicate (nlspnmodel.py:209-224)");
+        L = make_bwd<3, 3, 8, 32, 1, 1, 1, false>(a, first);
+        return NLSPN_OK;
+    }
+    if (kh == 3 && kw == 3)
+        L = vec ? make_bwd<3, 3, 8, 32, 8, 8, 4, true>(a, first) : make_bwd<3, 3, 8, 32, 8, 8, 1, true>(a, first);
+    else if (kh == 1 && kw == 17)
+        L = vec ? make_bwd<1, 17, 8, 32, 8, 16, 4, true>(a, first) : make_bwd<1, 17, 8, 32, 8, 16, 1, true>(a, first);
+    else if (kh == 5 && kw == 5)
+        L = vec ? make_bwd<5, 5, 8, 32, 8, 8, 4, true>(a, first) : make_bwd<5, 5, 8, 32, 8, 8, 1, true>(a, first);
+    else
+        return fail(NLSPN_EUNSUPPORTED, "no backward instantiation for a %dx%d geometry (supported: 3x3, 5x5, 1x17)",
+                    kh, kw);
+    return NLSPN_OK;
+}
+
+template <int K>
+const void *bwd_final_fn() { return reinterpret_cast<const void *>(&bwd_final_kernel<K>); }
+
+const void *select_bwd_final(int K) {
+    switch (K) {
+        case 8: return bwd_final_fn<8>();
+        case 16: return bwd_final_fn<16>();
+        case 24: return bwd_final_fn<24>();
         default: return nullptr;
     }
 }
@@ -391,6 +441,90 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
     *mean_ms = (float)(sum / reps);
     *min_ms = mn;
     return NLSPN_OK;
+}
+
+size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw) {
+    const size_t N = (size_t)B * H * W, K = (size_t)kh * kw - 1;
+    return sizeof(float) * N * (2 + (K + 1) + 1);  // dL/df ping-pong, dL/daff (K+1 planes), dL/dconf'
+}
+
+int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
+                             const void *aff_raw, int64_t aff_bstride, const void *off_raw, int64_t off_bstride,
+                             const float *gamma, const void *pred_inter, const void *aff_norm, const void *conf_eff,
+                             const void *grad_pred, const void *grad_pred_inter, void *grad_pred_init,
+                             void *grad_conf, void *grad_aff_raw, void *grad_off_raw, float *grad_gamma,
+                             void *workspace, int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags,
+                             void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the backward is implemented for float32 storage");
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
+        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
+    if (!pred_init || !aff_raw || !gamma || !pred_inter || !aff_norm || !grad_pred_init || !grad_aff_raw || !workspace)
+        return fail(NLSPN_EINVAL, "null required pointer");
+    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    if (conf && (!conf_eff || !grad_conf)) return fail(NLSPN_EINVAL, "conf given without conf_eff / grad_conf");
+    if (off_raw && !grad_off_raw) return fail(NLSPN_EINVAL, "off_raw given without grad_off_raw");
+    const int K = kh * kw - 1;
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
+    if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
+    if (HW * (3LL * K + 4) * 4 > 0x7fffffffLL) return fail(NLSPN_EINVAL, "image too large for one batch item");
+    const void *ffn = select_bwd_final(K);
+    if (!ffn) return fail(NLSPN_EUNSUPPORTED, "no backward for K=%d (supported 8, 16, 24)", K);
+    hipStream_t s = as_stream(stream);
+    float *ws = static_cast<float *>(workspace);
+    float *gf[2] = {ws, ws + N};
+    float *g_aff = ws + 2 * N;
+    float *g_conf = ws + (2 + K + 1) * N;
+    NLSPN_HIP_TRY(hipMemsetAsync(workspace, 0, nlspn_backward_workspace_bytes(B, H, W, kh, kw), s));
+    if (off_raw) NLSPN_HIP_TRY(hipMemsetAsync(grad_off_raw, 0, sizeof(float) * 2 * K * N, s));
+    if (grad_gamma) NLSPN_HIP_TRY(hipMemsetAsync(grad_gamma, 0, sizeof(float), s));
+    const bool vec = (W % 4 == 0) && aligned(pred_init, 16) && aligned(pred_inter, 16) && aligned(conf, 16) &&
+                     aligned(conf_eff, 16) && aligned(dep, 16);
+    const float *pi = static_cast<const float *>(pred_inter);
+    int rc = NLSPN_OK;
+    for (int t = T; t >= 1; --t) {
+        const bool first = t == 1;
+        BwdArgs a{};
+        a.p_in = first ? static_cast<const float *>(pred_init) : pi + (size_t)(t - 2) * N;
+        a.p_out = pi + (size_t)(t - 1) * N;
+        a.conf = first ? static_cast<const float *>(conf) : (conf ? static_cast<const float *>(conf_eff) : nullptr);
+        a.conf_eff = conf ? static_cast<const float *>(conf_eff) : nullptr;
+        a.dep = static_cast<const float *>(dep);
+        a.aff = static_cast<const float *>(aff_norm);
+        a.off = static_cast<const float *>(off_raw);
+        a.g_pred = static_cast<const float *>(grad_pred);
+        a.g_inter = grad_pred_inter ? static_cast<const float *>(grad_pred_inter) + (size_t)(t - 1) * N : nullptr;
+        a.gf_read = gf[t & 1];
+        a.gf_write = gf[(t - 1) & 1];
+        a.g_aff = g_aff;
+        a.g_off = static_cast<float *>(grad_off_raw);
+        a.g_conf = conf ? g_conf : nullptr;
+        a.off_bs = off_bstride;
+        a.B = B; a.H = H; a.W = W;
+        a.last = t == T;
+        a.flags = flags;
+        BwdLaunch L;
+        if ((rc = select_bwd(a, kh, kw, off_raw != nullptr, vec, first, L))) return rc;
+        void *args[] = {&a};
+        NLSPN_HIP_TRY(hipLaunchKernel(L.fn, L.grid, L.block, args, 0, s));
+        if ((rc = check_launch("nlspn_propagate_backward step"))) return rc;
+    }
+    const float *pinit = static_cast<const float *>(pred_init), *pdep = static_cast<const float *>(dep),
+                *pconf = static_cast<const float *>(conf), *pce = static_cast<const float *>(conf_eff),
+                *praw = static_cast<const float *>(aff_raw), *gf0 = gf[0];
+    const float *cg_aff = g_aff, *cg_conf = g_conf;
+    float *gpi = static_cast<float *>(grad_pred_init), *gc = static_cast<float *>(grad_conf),
+          *gar = static_cast<float *>(grad_aff_raw);
+    long long abs_ = aff_bstride, hw = HW;
+    int b_ = B, k_ = kind;
+    unsigned fl = flags;
+    void *fargs[] = {&pinit, &pdep, &pconf, &pce, &praw, &abs_, (void *)&gamma, &gf0, &cg_aff, &cg_conf,
+                     &gpi, &gc, &gar, &grad_gamma, &hw, &b_, &k_, &fl};
+    NLSPN_HIP_TRY(hipLaunchKernel(ffn, dim3(elementwise_grid(N)), dim3(256), fargs, 0, s));
+    return check_launch("nlspn_propagate_backward final");
 }
 
 }  // extern "C"

@@ -13,8 +13,11 @@ per-batch strides are passed through, so the (B, 3K, H, W) head output can be
 sliced into offsets/affinities without a copy (nlspnmodel.py:304-305).
 Computation is fp32; storage may be fp32 or fp16.
 
-These functional ops are inference ops (not differentiable); the backward of
-the fused step is the next row of the build plan.
+propagate() is differentiable (float32 storage): its backward is the native
+nlspn_propagate_backward (DCN col2im/col2im_coord + the autograd of the blends,
+clamps and affinity normalisation), giving gradients for pred_init, confidence,
+the raw affinity, the raw offsets and gamma.  prop_step() and
+affinity_normalization() are inference building blocks.
 """
 from __future__ import annotations
 
@@ -80,13 +83,6 @@ def _gamma_f32(gamma) -> torch.Tensor:
         raise TypeError("gamma must be a device tensor (aff_scale_const)")
     g = gamma.detach().reshape(-1)[:1]
     return g if g.dtype == torch.float32 else g.float()
-
-
-def _no_grad_inputs(*ts) -> None:
-    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
-        raise NotImplementedError(
-            "the fused NLSPN propagation has no backward yet (build plan §8f rank 1); "
-            "call it under torch.no_grad() / in eval mode")
 
 
 # -------------------------------------------------------------- functional ops
@@ -207,27 +203,80 @@ def _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop
     return args, g
 
 
+class _PropagateFn(torch.autograd.Function):
+    """Autograd node for the whole propagation section.  Differentiable outputs:
+    pred and pred_inter.  aff (normalised), offset (inserted) and confidence
+    (blended) are returned for the output dict but marked non-differentiable."""
+
+    @staticmethod
+    def forward(ctx, pred_init, dep, confidence, aff, offset, gamma, prop_time, affinity, kernel, preserve_input,
+                always_clip, return_offset):
+        kh, kw = kernel_geometry(kernel)
+        outs = _alloc_outputs(pred_init, kh * kw - 1, prop_time, offset is not None and return_offset,
+                              confidence is not None)
+        args, _ = _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
+                                  preserve_input, always_clip, outs)
+        with torch.cuda.device(pred_init.device):
+            _lib.check(_lib.get().nlspn_propagate(*args, _stream(pred_init.device)))
+        ctx.cfg = (kh, kw, int(prop_time), affinity, preserve_input, always_clip)
+        ctx.save_for_backward(pred_init, dep, confidence, aff, offset, gamma, outs["pred_inter"], outs["aff"],
+                              outs["confidence"])
+        nd = [t for t in (outs["aff"], outs["offset"], outs["confidence"]) if t is not None]
+        ctx.mark_non_differentiable(*nd)
+        return outs["pred"], outs["pred_inter"], outs["aff"], outs["offset"], outs["confidence"]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_pred, g_inter, _g_aff, _g_off, _g_conf):
+        pred_init, dep, conf, aff, off, gamma, pred_inter, aff_norm, conf_eff = ctx.saved_tensors
+        kh, kw, T, affinity, preserve, clip = ctx.cfg
+        if pred_init.dtype != torch.float32:
+            raise NotImplementedError("the propagation backward is implemented for float32 storage")
+        B, _, H, W = pred_init.shape
+        K = kh * kw - 1
+        dev = pred_init.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        g_pred = None if g_pred is None else g_pred.contiguous()
+        g_inter = None if g_inter is None else g_inter.contiguous()
+        g_pi = torch.empty((B, 1, H, W), **f32)
+        g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
+        g_aff = torch.empty((B, K, H, W), **f32)
+        g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+        g_gamma = torch.zeros(1, **f32)
+        lib = _lib.get()
+        ws = torch.empty(lib.nlspn_backward_workspace_bytes(B, H, W, kh, kw) // 4, **f32)
+        g = _gamma_f32(gamma)
+        flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
+        abs_ = _planes("aff", aff, B, K, H, W)
+        obs = _planes("offset", off, B, 2 * K, H, W) if off is not None else 0
+        with torch.cuda.device(dev):
+            _lib.check(lib.nlspn_propagate_backward(
+                _lib.DTYPE_F32, _ptr(pred_init), _ptr(dep), _ptr(conf), _ptr(aff), abs_, _ptr(off), obs, _ptr(g),
+                _ptr(pred_inter), _ptr(aff_norm), _ptr(conf_eff), _ptr(g_pred), _ptr(g_inter), _ptr(g_pi),
+                _ptr(g_conf), _ptr(g_aff), _ptr(g_off), _ptr(g_gamma), _ptr(ws), B, H, W, kh, kw, T,
+                _lib.AFF_KINDS[affinity], flags, _stream(dev)))
+        g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype) if affinity == "TGASS" else None
+        return (g_pi, None, g_conf, g_aff, g_off, g_gamma) + (None,) * 6
+
+
 def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: Optional[torch.Tensor],
               aff: torch.Tensor, offset: Optional[torch.Tensor], gamma: torch.Tensor, *, prop_time: int = 18,
               affinity: str = "TGASS", kernel=(3, 3), preserve_input: bool = True, always_clip: bool = False,
               return_offset: bool = True) -> dict:
     """The propagation section of NLSPNModel.forward (nlspnmodel.py:323-381), fused:
-    1 prologue launch + prop_time iteration launches on the current stream.
+    prop_time launches on the current stream (the prologue rides in the first).
 
     aff: raw affinity (B, K, H, W); offset: raw offsets (B, 2K, H, W) or None;
     gamma: aff_scale_const (device tensor, read on the device).
     Returns {'pred', 'pred_inter' (list of prop_time (B,1,H,W) views), 'offset'
     (inserted, or None), 'aff' (normalised, K+1 taps), 'confidence' (blended, or None)}.
+    Differentiable in pred_init, confidence, aff, offset and gamma when autograd is on.
     """
-    kh, kw = kernel_geometry(kernel)
-    outs = _alloc_outputs(pred_init, kh * kw - 1, prop_time, offset is not None and return_offset,
-                          confidence is not None)
-    args, _ = _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
-                              preserve_input, always_clip, outs)
-    with torch.cuda.device(pred_init.device):
-        _lib.check(_lib.get().nlspn_propagate(*args, _stream(pred_init.device)))
-    return {"pred": outs["pred"], "pred_inter": list(outs["pred_inter"].unbind(0)), "offset": outs["offset"],
-            "aff": outs["aff"], "confidence": outs["confidence"], "pred_inter_tensor": outs["pred_inter"]}
+    pred, pred_inter, aff_o, off_o, conf_o = _PropagateFn.apply(
+        pred_init, dep, confidence, aff, offset, gamma, prop_time, affinity, kernel, preserve_input, always_clip,
+        return_offset)
+    return {"pred": pred, "pred_inter": list(pred_inter.unbind(0)), "offset": off_o, "aff": aff_o,
+            "confidence": conf_o, "pred_inter_tensor": pred_inter}
 
 
 class PropagationPlan:
@@ -306,13 +355,9 @@ class NLSPNPropagation(nn.Module):
             off, aff = None, off_aff
         if not a.conf_prop:
             confidence = None
-        if self.training:
-            _no_grad_inputs(pred_init, dep, off_aff, confidence, self.aff_scale_const)
-        with torch.no_grad():
-            out = propagate(pred_init.detach(), dep, None if confidence is None else confidence.detach(),
-                            aff.detach(), None if off is None else off.detach(), self.aff_scale_const,
-                            prop_time=a.prop_time, affinity=a.affinity, kernel=(self.kh, self.kw),
-                            preserve_input=a.preserve_input, always_clip=a.always_clip)
+        out = propagate(pred_init, dep, confidence, aff, off, self.aff_scale_const, prop_time=a.prop_time,
+                        affinity=a.affinity, kernel=(self.kh, self.kw), preserve_input=a.preserve_input,
+                        always_clip=a.always_clip)
         return {"pred": out["pred"], "pred_init": pred_init, "pred_inter": out["pred_inter"],
                 "offset": out["offset"], "aff": out["aff"], "gamma": self.aff_scale_const.data,
                 "confidence": out["confidence"]}

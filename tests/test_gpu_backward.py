@@ -1,0 +1,104 @@
+"""GPU parity of the propagation backward (nlspn_propagate_backward through torch
+autograd) against the oracle's backward in fp64 on the same fp32 inputs; the
+oracle backward is itself pinned by finite differences (test_oracle_backward.py).
+
+Tolerance: relative L2 error per gradient tensor <= 1e-4 (dL/df is scattered
+with float atomics, as the reference's col2im, so the last bits depend on
+arrival order; the fp32 vs fp64 difference over T iterations dominates)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from nlspn_eccv20_amd import NLSPNPropagation, propagate
+from nlspn_eccv20_amd.synthetic import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def run_case(oracle, B, H, W, kh=3, kw=3, T=6, kind="TGASS", offset=True, conf=True, preserve=True, clip=False,
+             sigma=2.0, seed=0, inter=True):
+    K = kh * kw - 1
+    gamma = {"TGASS": 0.5 * K, "TC": float(K)}.get(kind, 1.0)
+    s = synth(B, H, W, K, seed=seed, density=0.05, off_sigma=sigma, offset=offset)
+    rng = np.random.default_rng(seed + 1)
+    wp = rng.standard_normal((B, 1, H, W)).astype(np.float32)
+    wi = rng.standard_normal((T, B, 1, H, W)).astype(np.float32) if inter else None
+    t = lambda x, rg=True: torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(rg)  # noqa: E731
+    off_aff = t(s["off_aff"])
+    pi, cf = t(s["pred_init"]), t(s["conf"]) if conf else None
+    g = torch.tensor([gamma], device=DEV, requires_grad=kind == "TGASS")
+    aff = off_aff[:, 2 * K:] if offset else off_aff
+    off = off_aff[:, :2 * K] if offset else None
+    o = propagate(pi, t(s["dep"], False), cf, aff, off, g, prop_time=T, affinity=kind, kernel=(kh, kw),
+                  preserve_input=preserve, always_clip=clip)
+    loss = (o["pred"] * t(wp, False)).sum()
+    if inter:
+        loss = loss + (o["pred_inter_tensor"] * t(wi, False)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    f64 = lambda x: None if x is None else x.astype(np.float64)  # noqa: E731
+    ref = oracle.propagate_backward(
+        f64(s["pred_init"]), f64(s["dep"]), f64(s["conf"]) if conf else None,
+        f64(s["off_aff"][:, 2 * K:] if offset else s["off_aff"]), f64(s["off_aff"][:, :2 * K]) if offset else None,
+        float(np.float32(gamma)), f64(wp), f64(wi), kind=kind, kh=kh, kw=kw, prop_time=T, preserve_input=preserve,
+        always_clip=clip)
+    ga = off_aff.grad.cpu().numpy()
+    got = {"pred_init": pi.grad.cpu().numpy(), "aff": ga[:, 2 * K:] if offset else ga}
+    if offset:
+        got["offset"] = ga[:, :2 * K]
+    if conf:
+        got["confidence"] = cf.grad.cpu().numpy()
+    for k, v in got.items():
+        e = rel(v, ref[k])
+        assert e < 1e-4, (k, e)
+    if kind == "TGASS":
+        assert abs(g.grad.item() - ref["gamma"]) <= 1e-4 * max(1.0, abs(ref["gamma"])), (g.grad.item(), ref["gamma"])
+    return got
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),
+    dict(clip=True),
+    dict(preserve=False),
+    dict(conf=False),
+    dict(kind="ASS"),
+    dict(kind="TC"),
+    dict(kind="AS"),
+    dict(offset=False),
+    dict(inter=False),
+    dict(sigma=8.0, seed=4),            # many taps beyond the LDS window (global scatter path)
+    dict(W=45, H=19),                   # scalar staging, partial tiles
+    dict(kh=1, kw=17, H=16, W=48),      # K=16 geometry
+    dict(kh=5, kw=5, H=16, W=32),       # K=24
+])
+def test_backward_vs_oracle(oracle, kw):
+    args = dict(B=2, H=24, W=40)
+    args.update(kw)
+    run_case(oracle, **args)
+
+
+def test_backward_full_T18(oracle):
+    run_case(oracle, B=1, H=40, W=64, T=18, seed=9)
+
+
+def test_module_trains(oracle):
+    """The drop-in module in training mode: gradients reach off_aff, pred_init, confidence and gamma."""
+    args = types.SimpleNamespace(prop_kernel=3, affinity="TGASS", affinity_gamma=0.5, prop_time=4,
+                                 preserve_input=True, always_clip=False, conf_prop=True, offset=True)
+    m = NLSPNPropagation(args).to(DEV).train()
+    s = synth(2, 20, 32, 8, seed=2)
+    t = lambda x: torch.from_numpy(x).to(DEV).requires_grad_(True)  # noqa: E731
+    pi, cf, oa = t(s["pred_init"]), t(s["conf"]), t(s["off_aff"])
+    out = m(pi, torch.from_numpy(s["dep"]).to(DEV), oa, cf)
+    out["pred"].mean().backward()
+    assert all(x.grad is not None and torch.isfinite(x.grad).all() for x in (pi, cf, oa))
+    assert m.aff_scale_const.grad is not None and m.w.grad is None
