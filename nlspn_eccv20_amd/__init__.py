@@ -8,10 +8,12 @@ with a torch-facing mirror of the reference interface:
   propagation.PropagationPlan   — the whole section as one native hipGraph
   propagation.NLSPNPropagation  — nn.Module with the reference's state_dict names
   dcn                           — `DCN`-compatible module (seam 2)
+  model.NLSPNModel              — the whole reference model (seam 1), heads on MIOpen
 """
+from .model import NLSPNModel
 from .propagation import (NLSPNPropagation, PropagationPlan, affinity_normalization, kernel_geometry,
                           off_insert, prop_step, propagate)
 
-__all__ = ["NLSPNPropagation", "PropagationPlan", "affinity_normalization", "kernel_geometry", "off_insert",
+__all__ = ["NLSPNModel", "NLSPNPropagation", "PropagationPlan", "affinity_normalization", "kernel_geometry", "off_insert",
            "prop_step", "propagate"]
 __version__ = "0.1.0"

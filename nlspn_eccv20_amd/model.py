@@ -1,0 +1,336 @@
+"""Seam 1 of the drop-in: NLSPNModel with the reference's module tree and state_dict
+keys, its encoder/decoder on stock PyTorch-ROCm (MIOpen convolutions) and its
+propagation section on the MI355X kernels.
+
+Mirrors XJTUXYC/NLSPN_ECCV20:
+  src/model/nlspnmodel.py:23-159   NLSPNModel.__init__ (same attribute names / order)
+  src/model/nlspnmodel.py:271-383  forward (encoder, heads, propagation, output dict)
+  src/model/nlspnmodel.py:386-462  ConvGRU, S2D
+  src/model/common.py:27-91        get_resnet18/34, conv_bn_relu, convt_bn_relu
+The ResNet stages (`conv2..conv4` = torchvision resnet layer1..layer3) are built
+here with torchvision's module naming (conv1/bn1/relu/conv2/bn2/downsample), since
+torchvision is not part of this stack; reference checkpoints load unchanged.
+
+Propagation: without the ConvGRU the whole section is one fused, differentiable
+op (propagate: prop_time launches).  With use_GRU (the reference's forced default,
+src/config.py:225-228) the affinity is re-estimated after every iteration
+(nlspnmodel.py:365-373), so each iteration is prop_step + affinity_normalization
+around the GRU's MIOpen convolutions; that mode is inference-only this round.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .propagation import affinity_normalization, kernel_geometry, prop_step, propagate
+
+__all__ = ["NLSPNModel", "ConvGRU", "S2D", "conv_bn_relu", "convt_bn_relu", "get_resnet18", "get_resnet34", "get"]
+
+model_path = {"resnet18": "pretrained/resnet18.pth", "resnet34": "pretrained/resnet34.pth"}
+
+
+# ---------------------------------------------------------------- common.py
+def conv_bn_relu(ch_in, ch_out, kernel, stride=1, bn=True, relu=True, zero_init=False):
+    """common.py:44-67: Sequential(conv[, bn][, relu])."""
+    assert (kernel % 2) == 1, "only odd kernel is supported but kernel = {}".format(kernel)
+    layers = [nn.Conv2d(ch_in, ch_out, kernel, stride, (kernel - 1) // 2, bias=not bn)]
+    if zero_init:
+        layers[0].weight.data.zero_()
+        if not bn:
+            layers[0].bias.data.zero_()
+    if bn:
+        layers.append(nn.BatchNorm2d(ch_out))
+    if relu:
+        layers.append(nn.ReLU(inplace=True))
+    return nn.Sequential(*layers)
+
+
+def convt_bn_relu(ch_in, ch_out, kernel, stride=1, padding=0, output_padding=0, bn=True, relu=True,
+                  zero_init=False):
+    """common.py:70-91: Sequential(convT[, bn][, relu])."""
+    assert (kernel % 2) == 1, "only odd kernel is supported but kernel = {}".format(kernel)
+    layers = [nn.ConvTranspose2d(ch_in, ch_out, kernel, stride, padding, output_padding, bias=not bn)]
+    if zero_init:
+        layers[0].weight.data.zero_()
+        if not bn:
+            layers[0].bias.data.zero_()
+    if bn:
+        layers.append(nn.BatchNorm2d(ch_out))
+    if relu:
+        layers.append(nn.ReLU(inplace=True))
+    return nn.Sequential(*layers)
+
+
+class BasicBlock(nn.Module):
+    """ResNet basic block with torchvision's parameter names."""
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
+
+
+class _ResNetStages(nn.Module):
+    """layer1..layer3 of a torchvision-style ResNet (the stages NLSPN keeps, nlspnmodel.py:45-52)."""
+
+    def __init__(self, blocks):
+        super().__init__()
+        self.inplanes = 64
+        self.layer1 = self._make(64, blocks[0], 1)
+        self.layer2 = self._make(128, blocks[1], 2)
+        self.layer3 = self._make(256, blocks[2], 2)
+        for m in self.modules():  # torchvision's initialisation
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make(self, planes, n, stride):
+        down = None
+        if stride != 1 or self.inplanes != planes:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes, 1, stride, bias=False), nn.BatchNorm2d(planes))
+        layers = [BasicBlock(self.inplanes, planes, stride, down)]
+        self.inplanes = planes
+        layers += [BasicBlock(planes, planes) for _ in range(1, n)]
+        return nn.Sequential(*layers)
+
+
+def _get_resnet(name, blocks, pretrained):
+    net = _ResNetStages(blocks)
+    if pretrained:  # common.py:27-42: torchvision resnet state_dict from pretrained/<name>.pth
+        sd = torch.load(model_path[name], map_location="cpu", weights_only=True)
+        net.load_state_dict({k: v for k, v in sd.items() if k.split(".")[0] in ("layer1", "layer2", "layer3")})
+    return net
+
+
+def get_resnet18(pretrained=True):
+    return _get_resnet("resnet18", (2, 2, 2), pretrained)
+
+
+def get_resnet34(pretrained=True):
+    return _get_resnet("resnet34", (3, 4, 6), pretrained)
+
+
+# ---------------------------------------------------------------- nlspnmodel.py
+class ConvGRU(nn.Module):
+    """nlspnmodel.py:386-403."""
+
+    def __init__(self, args):
+        super().__init__()
+        c = args.GRU_hidden_dim + args.GRU_input_dim
+        self.convz = nn.Conv2d(c, args.GRU_hidden_dim, 3, padding=1)
+        self.convr = nn.Conv2d(c, args.GRU_hidden_dim, 3, padding=1)
+        self.convq = nn.Conv2d(c, args.GRU_hidden_dim, 3, padding=1)
+
+    def forward(self, h, x):
+        hx = torch.cat([h, x], dim=1)
+        z = torch.sigmoid(self.convz(hx))
+        r = torch.sigmoid(self.convr(hx))
+        q = torch.tanh(self.convq(torch.cat([r * h, x], dim=1)))
+        return (1 - z) * h + z * q
+
+
+class S2D(nn.Module):
+    """nlspnmodel.py:406-462 (min/max-pool pyramid sparse-depth encoder)."""
+
+    def __init__(self):
+        super().__init__()
+        self.min_pool_sizes = [3, 5, 7, 9]
+        self.max_pool_sizes = [11, 13]
+        # plain lists, as in the reference: the pools carry no parameters or state_dict keys
+        self.min_pools = [nn.MaxPool2d(kernel_size=s, stride=1, padding=s // 2) for s in self.min_pool_sizes]
+        self.max_pools = [nn.MaxPool2d(kernel_size=s, stride=1, padding=s // 2) for s in self.max_pool_sizes]
+        in_channels = len(self.min_pool_sizes) + len(self.max_pool_sizes)
+        self.pool_convs = nn.Sequential(conv_bn_relu(in_channels, 8, kernel=1, stride=1, bn=False),
+                                        conv_bn_relu(8, 16, kernel=1, stride=1, bn=False))
+        self.conv = conv_bn_relu(16 + 1, 32, kernel=3, stride=1, bn=False)
+
+    def forward(self, dep):
+        pyr = []
+        for pool in self.min_pools:
+            z = -pool(torch.where(dep == 0, -999 * torch.ones_like(dep), -dep))
+            pyr.append(torch.where(z == 999, torch.zeros_like(dep), z))
+        for pool in self.max_pools:
+            pyr.append(pool(dep))
+        feat = self.pool_convs(torch.cat(pyr, dim=1))
+        return self.conv(torch.cat([feat, dep], dim=1))
+
+
+class NLSPNModel(nn.Module):
+    """Drop-in for src/model/nlspnmodel.py:23-383 (same constructor argument, same
+    submodule names, same forward(sample) -> dict)."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.args = args
+        kernel = getattr(args, "prop_kernel_hw", None) or args.prop_kernel
+        self.kh, self.kw = kernel_geometry(kernel)
+        self.num_neighbors = self.kh * self.kw - 1
+
+        self.conv1_rgb = conv_bn_relu(3, 32, kernel=3, stride=1, bn=False)
+        self.conv1_dep = conv_bn_relu(1, 32, kernel=3, stride=1, bn=False)
+        if args.network == "resnet18":
+            net = get_resnet18(not args.from_scratch)
+        elif args.network == "resnet34":
+            net = get_resnet34(not args.from_scratch)
+        else:
+            raise NotImplementedError
+        self.conv2, self.conv3, self.conv4 = net.layer1, net.layer2, net.layer3
+        del net
+        self.conv5 = conv_bn_relu(256, 256, kernel=3, stride=2)
+        self.dec4 = convt_bn_relu(256, 128, kernel=3, stride=2, padding=1, output_padding=1)
+        self.dec3 = convt_bn_relu(128 + 256, 64, kernel=3, stride=2, padding=1, output_padding=1)
+        self.dec2 = convt_bn_relu(64 + 128, 64, kernel=3, stride=2, padding=1, output_padding=1)
+        self.id_dec1 = conv_bn_relu(64 + 64, 64, kernel=3, stride=1)
+        self.id_dec0 = conv_bn_relu(64 + 64, 1, kernel=3, stride=1, bn=False, relu=True)
+        self.off_aff_dec1 = conv_bn_relu(64 + 64, 64, kernel=3, stride=1)
+        nout = 3 * self.num_neighbors if args.offset else self.num_neighbors
+        self.off_aff_dec0 = conv_bn_relu(64 + 64, nout, kernel=3, stride=1, bn=False, relu=False,
+                                         zero_init=args.zero_init_aff)
+        if args.conf_prop:
+            self.cf_dec1 = conv_bn_relu(64 + 64, 64, kernel=3, stride=1)
+            self.cf_dec0 = nn.Sequential(nn.Conv2d(64 + 64, 1, kernel_size=3, stride=1, padding=1), nn.Sigmoid())
+        self.ch_f = 1
+        self.idx_ref = self.num_neighbors // 2
+        if args.affinity in ("AS", "ASS", "TC", "TGASS"):
+            if args.affinity == "TC":
+                self.aff_scale_const = nn.Parameter(self.num_neighbors * torch.ones(1), requires_grad=False)
+            elif args.affinity == "TGASS":
+                self.aff_scale_const = nn.Parameter(args.affinity_gamma * self.num_neighbors * torch.ones(1))
+            else:
+                self.aff_scale_const = nn.Parameter(torch.ones(1), requires_grad=False)
+        else:
+            raise NotImplementedError
+        self.w = nn.Parameter(torch.ones((self.ch_f, 1, self.kh, self.kw)), requires_grad=False)
+        self.b = nn.Parameter(torch.zeros(self.ch_f), requires_grad=False)
+        self.w_conf = nn.Parameter(torch.ones((1, 1, 1, 1)), requires_grad=False)
+        self.stride, self.padding, self.dilation = 1, (self.kh - 1) // 2, 1
+        self.groups, self.deformable_groups, self.im2col_step = self.ch_f, 1, 64
+        if args.use_GRU:
+            self.GRU = ConvGRU(args)
+            self.encode_aff = nn.Sequential(
+                conv_bn_relu(self.num_neighbors + 1, 16, kernel=3, stride=2, bn=False),
+                conv_bn_relu(16, 2 * args.GRU_hidden_dim, kernel=3, stride=2, bn=False),
+                conv_bn_relu(2 * args.GRU_hidden_dim, args.GRU_hidden_dim, kernel=3, stride=2, bn=False, relu=False),
+                nn.Tanh())
+            self.encode_dep = nn.Sequential(
+                conv_bn_relu(1, 16, kernel=3, stride=2, bn=False),
+                conv_bn_relu(16, 2 * args.GRU_input_dim, kernel=3, stride=2, bn=False),
+                conv_bn_relu(2 * args.GRU_input_dim, args.GRU_input_dim, kernel=3, stride=2, bn=False))
+            self.decode_aff = nn.Sequential(
+                convt_bn_relu(args.GRU_hidden_dim, 2 * args.GRU_hidden_dim, kernel=3, stride=2, padding=1,
+                              output_padding=1, bn=False),
+                convt_bn_relu(2 * args.GRU_hidden_dim, 16, kernel=3, stride=2, padding=1, output_padding=1,
+                              bn=False),
+                convt_bn_relu(16, self.num_neighbors, kernel=3, stride=2, padding=1, output_padding=1, bn=False,
+                              relu=False, zero_init=args.zero_init_aff))
+        if args.use_S2D:
+            self.S2D = S2D()
+        params = nn.ParameterList([p for p in self.parameters() if p.requires_grad])
+        self.param_groups = [{"params": params, "lr": args.lr}]
+
+    @staticmethod
+    def _concat(fd, fe, dim=1):
+        """nlspnmodel.py:161-177: crop decoder padding, then concatenate."""
+        _, _, Hd, Wd = fd.shape
+        _, _, He, We = fe.shape
+        if Hd > He:
+            fd = fd[:, :, :He, :]
+        if Wd > We:
+            fd = fd[:, :, :, :We]
+        return torch.cat((fd, fe), dim=dim)
+
+    def heads(self, sample):
+        """Encoder + decoder heads, nlspnmodel.py:272-315: (pred_init, off_aff, confidence)."""
+        rgb, dep = sample["rgb"], sample["dep"]
+        fe1_rgb = self.conv1_rgb(rgb)
+        fe1_dep = self.S2D(dep) if self.args.use_S2D else self.conv1_dep(dep)
+        fe1 = torch.cat((fe1_rgb, fe1_dep), dim=1)
+        fe2 = self.conv2(fe1)
+        fe3 = self.conv3(fe2)
+        fe4 = self.conv4(fe3)
+        fe5 = self.conv5(fe4)
+        fd4 = self.dec4(fe5)
+        fd3 = self.dec3(self._concat(fd4, fe4))
+        fd2 = self.dec2(self._concat(fd3, fe3))
+        id_fd1 = self.id_dec1(self._concat(fd2, fe2))
+        pred_init = self.id_dec0(self._concat(id_fd1, fe1))
+        off_aff_fd1 = self.off_aff_dec1(self._concat(fd2, fe2))
+        off_aff = self.off_aff_dec0(self._concat(off_aff_fd1, fe1))
+        confidence = None
+        if self.args.conf_prop:
+            cf_fd1 = self.cf_dec1(self._concat(fd2, fe2))
+            confidence = self.cf_dec0(self._concat(cf_fd1, fe1))
+        return pred_init, off_aff, confidence
+
+    def _aff_head(self, aff_feat):
+        """nlspnmodel.py:228-234 (+ the _clip_as crop :237-250)."""
+        aff = self.decode_aff(aff_feat)
+        aff = aff[:, :, :self.args.patch_height, :self.args.patch_width].contiguous()
+        return affinity_normalization(aff, self.aff_scale_const, self.args.affinity)
+
+    def forward(self, sample):
+        pred_init, off_aff, confidence = self.heads(sample)
+        return self.propagate_heads(pred_init, off_aff, confidence, sample["dep"])
+
+    def propagate_heads(self, pred_init, off_aff, confidence, dep):
+        """The propagation section, nlspnmodel.py:303-383, on the heads' outputs."""
+        a = self.args
+        assert self.ch_f == pred_init.shape[1]
+        K = self.num_neighbors
+        off = off_aff[:, :2 * K] if a.offset else None
+        aff = off_aff[:, 2 * K:] if a.offset else off_aff
+        if not a.use_GRU:
+            o = propagate(pred_init, dep if a.preserve_input else None, confidence if a.conf_prop else None, aff,
+                          off, self.aff_scale_const, prop_time=a.prop_time, affinity=a.affinity,
+                          kernel=(self.kh, self.kw), preserve_input=a.preserve_input, always_clip=a.always_clip)
+            return {"pred": o["pred"], "pred_init": pred_init, "pred_inter": o["pred_inter"], "offset": o["offset"],
+                    "aff": o["aff"], "gamma": self.aff_scale_const.data, "confidence": o["confidence"]}
+        return self._forward_gru(pred_init, dep, off, aff, confidence)
+
+    def _forward_gru(self, pred_init, dep, off, aff_raw, confidence):
+        """nlspnmodel.py:323-383 with use_GRU: the affinity is re-estimated after every
+        iteration (:365-373).  Iteration 1 runs the fused first step (prologue inside);
+        later iterations run prop_step on the GRU's freshly normalised affinity."""
+        a = self.args
+        if torch.is_grad_enabled() and self.training:
+            raise NotImplementedError("GRU-mode propagation is inference-only this round (build plan §8f rank 2)")
+        with torch.no_grad():
+            o = propagate(pred_init, dep if a.preserve_input else None, confidence if a.conf_prop else None,
+                          aff_raw, off, self.aff_scale_const, prop_time=1, affinity=a.affinity,
+                          kernel=(self.kh, self.kw), preserve_input=a.preserve_input, always_clip=a.always_clip)
+            new_pred = o["pred_inter"][0]
+            aff, conf_eff = o["aff"], o["confidence"]
+            list_pred = [new_pred]
+            for k in range(2, a.prop_time + 1):
+                dep_feat = self.encode_dep(new_pred / a.max_depth)
+                if k == 2:
+                    aff_feat = self.encode_aff(aff)
+                aff_feat = self.GRU(h=aff_feat, x=dep_feat)
+                aff = self._aff_head(aff_feat)
+                new_pred = prop_step(new_pred, conf_eff, dep if a.preserve_input else None, aff, off,
+                                     kernel=(self.kh, self.kw), offset_layout="raw", preserve_input=a.preserve_input,
+                                     always_clip=a.always_clip)
+                list_pred.append(new_pred)
+            pred = new_pred if a.always_clip else torch.clamp(new_pred, min=0)
+        return {"pred": pred, "pred_init": pred_init, "pred_inter": list_pred, "offset": o["offset"], "aff": aff,
+                "gamma": self.aff_scale_const.data, "confidence": conf_eff}
+
+
+def get(args):
+    """Registry seam, src/model/__init__.py:17-22: model.get(args) -> model class."""
+    if (args.model_name + "Model").lower() != "nlspnmodel":
+        raise NotImplementedError(args.model_name)
+    return NLSPNModel

@@ -181,6 +181,27 @@ def main():
          gamma=m.aff_scale_const.detach().reshape(1), pred=o["pred"],
          pred_inter_last=o["pred_inter"][-1], confidence=o["confidence"])
 
+    # 6) NLSPNModel state_dict names/shapes (checkpoint compatibility of the drop-in).
+    #    The ResNet stages come from torchvision (absent): a stub returns empty
+    #    layer1..layer3 so only the keys the reference itself defines are recorded.
+    tv = sys.modules["torchvision"]
+    tv.models = types.SimpleNamespace(
+        resnet18=lambda pretrained=False: types.SimpleNamespace(layer1=nn.Sequential(), layer2=nn.Sequential(),
+                                                                 layer3=nn.Sequential()),
+        resnet34=lambda pretrained=False: types.SimpleNamespace(layer1=nn.Sequential(), layer2=nn.Sequential(),
+                                                                 layer3=nn.Sequential()))
+    keys = {}
+    for tag, kw in (("gru_s2d_offset", dict(offset=True, use_GRU=True, use_S2D=True, conf_prop=True)),
+                    ("plain", dict(offset=False, use_GRU=False, use_S2D=False, conf_prop=True))):
+        args = types.SimpleNamespace(prop_kernel=3, affinity="TGASS", affinity_gamma=0.5, prop_time=18,
+                                     preserve_input=True, always_clip=False, network="resnet34", from_scratch=True,
+                                     zero_init_aff=True, GRU_hidden_dim=128, GRU_input_dim=128, lr=1e-3, **kw)
+        torch.manual_seed(0)
+        m = nl.NLSPNModel(args)
+        keys[tag] = {k: list(v.shape) for k, v in m.state_dict().items()}
+    with open(os.path.join(a.out, "state_dict_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0, sort_keys=True)
+
     with open(os.path.join(a.out, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     total = sum(os.path.getsize(os.path.join(a.out, n + ".npz")) for n in manifest["cases"])
