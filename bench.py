@@ -18,6 +18,9 @@ Extra JSON objects:
                  (S*(4+3K) per pixel) / mean kernel duration from
                  dispatch-recorded HIP events (nlspn_time_prop_step) on this
                  stream; traffic from profiles/pmc_<config>.json when present.
+  backward     — (fp32 configs) forward+backward of the section through autograd
+                 (nlspn_propagate + nlspn_propagate_backward), ms per step and per
+                 iteration, HIP-event timed on this stream; not part of `value`.
   cpu_baseline — the C oracle (kind "port"; the reference has no CPU DCN path)
                  on the same workload, rank 0, N=1.
 """
@@ -38,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from nlspn_eccv20_amd import _lib  # noqa: E402
-from nlspn_eccv20_amd.propagation import PropagationPlan, _ptr, _stream  # noqa: E402
+from nlspn_eccv20_amd.propagation import PropagationPlan, _ptr, _stream, propagate  # noqa: E402
 from nlspn_eccv20_amd.sharding import max_over_ranks  # noqa: E402
 from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
 
@@ -70,6 +73,8 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--no-backward", action="store_true")
+    ap.add_argument("--backward-steps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -88,6 +93,44 @@ def kernel_time(plan, inputs, cfg, reps, dev):
         cfg["kernel"][0], cfg["kernel"][1], _lib.PRESERVE_INPUT, reps, _stream(dev),
         ctypes.byref(mean_ms), ctypes.byref(min_ms)))
     return mean_ms.value, min_ms.value
+
+
+def backward_timing(inputs, cfg, steps):
+    """Forward+backward of the whole section (training step of the propagation), with
+    gradients for pred_init, confidence, the (B, 3K, H, W) head output and gamma."""
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    pi = inputs["pred_init"].detach().clone().requires_grad_(True)
+    cf = inputs["conf"].detach().clone().requires_grad_(True)
+    oa = torch.cat([inputs["off"], inputs["aff"]], 1).detach().requires_grad_(True)
+    g = inputs["gamma"].detach().clone().requires_grad_(True)
+    gp = torch.randn_like(pi)
+
+    def fwd():
+        return propagate(pi, inputs["dep"], cf, oa[:, 2 * K:], oa[:, :2 * K], g, prop_time=cfg["T"],
+                         kernel=cfg["kernel"])
+
+    def train_step():
+        torch.autograd.backward(fwd()["pred"], gp)
+
+    for _ in range(3):
+        train_step()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    torch.cuda.synchronize()
+    e[0].record()
+    for _ in range(steps):
+        train_step()
+    e[1].record()
+    with torch.no_grad():
+        e[2].record()
+        for _ in range(steps):
+            fwd()
+        e[3].record()
+    torch.cuda.synchronize()
+    fb = e[0].elapsed_time(e[1]) / steps
+    fo = e[2].elapsed_time(e[3]) / steps
+    return {"ms_fwd_bwd_per_step": round(fb, 4), "ms_fwd_per_step": round(fo, 4),
+            "ms_bwd_per_iter": round((fb - fo) / cfg["T"], 5), "steps": steps,
+            "note": "eager autograd (not graph-replayed); bwd = fwd+bwd - fwd"}
 
 
 def cpu_baseline(cfg, s, reps):
@@ -184,6 +227,8 @@ def main():
                      "kernel_ms_mean": round(kmean, 5), "kernel_ms_min": round(kmin, 5)},
         "gpu_event_ms_per_step": round(gpu_ms / a.steps, 4),
     }
+    if cfg["dtype"] == "f32" and not a.no_backward:
+        out["backward"] = backward_timing(inputs, cfg, a.backward_steps)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, s, a.cpu_reps)
     plan.close()

@@ -10,9 +10,13 @@
 // the confidence product, blends, clamps, _aff_insert and the affinity normalisation.
 //
 // One launch per iteration, t = T..1 (bwd_step_kernel), then one finishing
-// launch (bwd_final_kernel):
+// elementwise launch (bwd_final_kernel):
 //   * the iteration's output pixel owns its dL/d(affinity) and dL/d(offset)
-//     accumulators (plain read-modify-write across the T launches, no atomics);
+//     accumulators (plain read-modify-write across the T launches, no atomics;
+//     step T initialises them, so nothing is cleared beforehand); dL/d(affinity)
+//     is kept as G_k = dL/daff_k - dL/daff_ref (K planes, _aff_insert folded in);
+//   * step 1 finishes each pixel's affinity gradient in place: the normalisation
+//     backward runs on the final G and writes grad_aff_raw directly;
 //   * the scatter of dL/df_{t-1} to the 4 bilinear corners of every tap goes to an
 //     LDS window (ds_add_f32) covering the tile + halo; the window is flushed once
 //     with global float atomics (non-zero in-image cells only) and taps that leave
@@ -38,16 +42,106 @@ struct BwdArgs {
     const float *g_inter;   // dL/dpred_inter[t-1] or null
     float *gf_read;         // dL/df_t   (scattered by step t+1); zeroed after use
     float *gf_write;        // dL/df_{t-1} (scattered here)
-    float *g_aff;           // (K+1) planes per item, accumulated
-    float *g_off;           // 2K planes per item (raw layout), accumulated
+    float *g_aff;           // K planes per item: G_k = dL/daff_k - dL/daff_ref, accumulated
+    float *g_off;           // 2K planes per item (raw layout), accumulated = grad_off_raw
     float *g_conf;          // dL/dconf' plane, accumulated (null iff conf null)
     long long off_bs;
     int B, H, W, tiles_x, tiles_y;
-    int last;               // t == T
+    int last;               // t == T: accumulators are initialised, not read
     unsigned flags;
+    // FIRST only: affinity-normalisation backward fused in (per pixel, G final)
+    const float *aff_raw;   // raw head affinity, K planes per item at aff_raw_bs
+    long long aff_raw_bs;
+    const float *gamma;
+    float *grad_aff_raw;    // K planes per item, contiguous
+    float *gamma_part;      // one partial dL/dgamma per workgroup (TGASS), or null
+    int kind;
 };
 
-template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET, bool FIRST>
+__device__ __forceinline__ float bld(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+__device__ __forceinline__ void bst(rsrc_t r, unsigned vo, unsigned so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+}
+
+// Bilinear corners of f_{t-1} at (hs, ws) (caller checked validity): from the LDS
+// window when the 2x2 footprint lies inside it, else from global memory with the
+// reference's per-corner checks (.cuh:24-54).
+template <bool FIRST, int WH, int WW>
+__device__ __forceinline__ bool tap_corners(float hs, float ws, int wy0, int wx0, int H, int W, const float *win,
+                                            rsrc_t rp, rsrc_t rc, rsrc_t rd, bool has_conf, bool preserve, bool clip,
+                                            int &hl, int &wl, float (&v)[4]) {
+    hl = (int)floorf(hs);
+    wl = (int)floorf(ws);
+    const int ry = hl - wy0, rx = wl - wx0;
+    if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
+        const float *s = &win[ry * WW + rx];
+        v[0] = s[0]; v[1] = s[1]; v[2] = s[WW]; v[3] = s[WW + 1];
+        return true;
+    }
+    constexpr unsigned ES = 4;
+    const int r0 = hl * W, r1 = (hl + 1) * W;
+    v[0] = (hl >= 0 && wl >= 0) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + wl) * ES) : 0.f;
+    v[1] = (hl >= 0 && wl + 1 <= W - 1) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + wl + 1) * ES) : 0.f;
+    v[2] = (hl + 1 <= H - 1 && wl >= 0) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + wl) * ES) : 0.f;
+    v[3] = (hl + 1 <= H - 1 && wl + 1 <= W - 1) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + wl + 1) * ES) : 0.f;
+    return false;
+}
+
+// Backward of _affinity_normalization + _aff_insert for one pixel (nlspnmodel.py:
+// 179-201, :261-269): G_k = dL/daff_k - dL/daff_ref (aff_ref = 1 - sum aff_k);
+//   u = tanh(a)/(gamma+1e-8) [TGASS] | tanh(a)/gamma [TC] | a [AS/ASS];
+//   s = sum|u| + 1e-4, s = 1 where s < 1 [ASS/TGASS; no gradient there]; aff = u/s [not TC].
+template <int K>
+__device__ __forceinline__ float aff_norm_backward(const float (&G)[K], const float (&ar)[K], float gamma, int kind,
+                                                   float (&ga)[K]) {
+    float u[K], th[K], s = 0.f, dot = 0.f, gsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        th[k] = tanhf(ar[k]);
+        u[k] = kind == kAffTC ? th[k] / gamma : (kind == kAffTGASS ? th[k] / (gamma + 1e-8f) : ar[k]);
+        s += fabsf(u[k]);
+    }
+    s = s + 1e-4f;
+    const bool clamped = (kind == kAffASS || kind == kAffTGASS) && s < 1.0f;
+    const float se = clamped ? 1.0f : s;
+#pragma unroll
+    for (int k = 0; k < K; ++k) dot += G[k] * u[k];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float gu;
+        if (kind == kAffTC) {
+            gu = G[k];
+        } else {
+            gu = G[k] / se;
+            if (!clamped) {
+                const float sg = u[k] > 0.f ? 1.f : (u[k] < 0.f ? -1.f : 0.f);
+                gu += -dot / (se * se) * sg;
+            }
+        }
+        float g = gu;
+        if (kind == kAffTC) {
+            g = gu * (1.f - th[k] * th[k]) / gamma;
+        } else if (kind == kAffTGASS) {
+            const float dd = gamma + 1e-8f;
+            g = gu * (1.f - th[k] * th[k]) / dd;
+            gsum += -gu * th[k] / (dd * dd);
+        }
+        ga[k] = g;
+    }
+    return gsum;
+}
+
+// One backward iteration.  Every global load of the step is issued before the
+// first store (the compiler cannot reorder a buffer load above a buffer store it
+// cannot prove disjoint, so a read-modify-write per plane would cost one memory
+// round trip each): window staging, the tap planes, the own-pixel planes and —
+// for K <= 8 — the dL/daff and dL/doffset accumulators.  Larger K accumulate in
+// registers and read-modify-write in chunks of 8 planes.
+// DIAG: diagnostic knobs for tools/bwd_bench (0 in the library; non-zero values
+// produce wrong gradients): 1 = no window flush, 4 = no accumulator read-modify-write.
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET, bool FIRST, int DIAG = 0>
 __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
@@ -60,8 +154,11 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     constexpr int WV = WW / SV, NV = WH * WV, SIT = (NV + NT - 1) / NT;
     constexpr int NC = WH * WW, CIT = (NC + NT - 1) / NT;
     constexpr unsigned ES = 4;
+    constexpr bool HOIST = K <= 8;
+    constexpr int KO = OFFSET ? 2 * K : 1;
     __shared__ __attribute__((aligned(16))) float win[NC];   // f_{t-1} over the window
-    __shared__ float gwin[NC];                              // scatter accumulator for dL/df_{t-1}
+    __shared__ unsigned long long gacc[NC];                 // scatter accumulator for dL/df_{t-1} (fixed point)
+    __shared__ float red[NT / 64], redm[NT / 64];
 
     const int H = a.H, W = a.W;
     const long long HW = (long long)H * W;
@@ -76,6 +173,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
+    const bool last = a.last != 0;
     const float *pbase = a.p_in + b * HW;
     const rsrc_t rp = make_rsrc(pbase);
     const rsrc_t rc = make_rsrc(has_conf ? a.conf + b * HW : pbase);
@@ -84,10 +182,9 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     const int ly = threadIdx.x / TW, lx = threadIdx.x % TW;
     const int y = y0 + ly, x = x0 + lx;
     const bool active = (y < H) && (x < W);
-    const unsigned pix = active ? (unsigned)(y * W + x) : 0u;
-    const unsigned vpix = pix * ES, plane_bytes = (unsigned)HW * ES;
+    const unsigned vpix = (active ? (unsigned)(y * W + x) : 0u) * ES, plane_bytes = (unsigned)HW * ES;
 
-    // ---- staging loads of the window (as in the forward), then own-pixel loads
+    // ---- 1. all loads: window staging, tap planes, own pixel, accumulators
     float sp[SIT][SV], sc[SIT][SV], sd[FIRST ? SIT : 1][SV];
     bool sin[SIT];
 #pragma unroll
@@ -105,30 +202,36 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
         if (has_conf) BVec<float, SV>::load(rc, q, 0u, sc[it]);
         if (FIRST && preserve) BVec<float, SV>::load(rd, q, 0u, sd[FIRST ? it : 0]);
     }
-    float av[K][1], dh[K][1], dw[K][1];
     const rsrc_t ra = make_rsrc(a.aff + b * (K + 1) * HW);
     const rsrc_t ro = make_rsrc(OFFSET ? a.off + b * a.off_bs : a.aff);
+    float av[K], dh[OFFSET ? K : 1], dw[OFFSET ? K : 1];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        BVec<float, 1>::load(ra, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, av[k]);
+        av[k] = bld(ra, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes);
         if (OFFSET) {
-            BVec<float, 1>::load(ro, vpix, (2u * k) * plane_bytes, dh[k]);
-            BVec<float, 1>::load(ro, vpix, (2u * k + 1) * plane_bytes, dw[k]);
+            dh[k] = bld(ro, vpix, (2u * k) * plane_bytes);
+            dw[k] = bld(ro, vpix, (2u * k + 1) * plane_bytes);
         }
     }
-    float dv[1] = {0.f}, gfr[1], pt[1] = {0.f}, ce[1] = {1.f}, gi[1] = {0.f}, gpr[1] = {0.f};
-    if (preserve) BVec<float, 1>::load(rd, vpix, 0u, dv);
-    BVec<float, 1>::load(make_rsrc(a.gf_read + b * HW), vpix, 0u, gfr);
-    if (has_conf) {
-        BVec<float, 1>::load(make_rsrc(a.p_out + b * HW), vpix, 0u, pt);
-        BVec<float, 1>::load(make_rsrc(a.conf_eff + b * HW), vpix, 0u, ce);
-    } else if (a.last && a.g_pred && !clip) {
-        BVec<float, 1>::load(make_rsrc(a.p_out + b * HW), vpix, 0u, pt);
-    }
-    if (a.g_inter) BVec<float, 1>::load(make_rsrc(a.g_inter + b * HW), vpix, 0u, gi);
-    if (a.last && a.g_pred) BVec<float, 1>::load(make_rsrc(a.g_pred + b * HW), vpix, 0u, gpr);
+    const rsrc_t rgc = make_rsrc(has_conf ? a.g_conf + b * HW : a.gf_read);
+    const rsrc_t rgf = make_rsrc(a.gf_read + b * HW);
+    float dv = 0.f, gfr = 0.f, pt = 0.f, ce = 1.f, gi = 0.f, gpr = 0.f, gcv = 0.f;
+    if (preserve) dv = bld(rd, vpix, 0u);
+    if (!last) gfr = bld(rgf, vpix, 0u);
+    if (has_conf || (last && a.g_pred && !clip)) pt = bld(make_rsrc(a.p_out + b * HW), vpix, 0u);
+    if (has_conf) ce = bld(make_rsrc(a.conf_eff + b * HW), vpix, 0u);
+    if (has_conf && !last) gcv = bld(rgc, vpix, 0u);
+    if (a.g_inter) gi = bld(make_rsrc(a.g_inter + b * HW), vpix, 0u);
+    if (last && a.g_pred) gpr = bld(make_rsrc(a.g_pred + b * HW), vpix, 0u);
+    const rsrc_t rga = make_rsrc(a.g_aff + b * K * HW);
+    const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * 2 * K * HW : a.g_aff);
+    float cG[K], cO[KO];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cG[k] = (HOIST && !last && !(DIAG & 4)) ? bld(rga, vpix, (unsigned)k * plane_bytes) : 0.f;
+#pragma unroll
+    for (int k = 0; k < KO; ++k) cO[k] = (OFFSET && HOIST && !last && !(DIAG & 4)) ? bld(rgo, vpix, (unsigned)k * plane_bytes) : 0.f;
 
-    // ---- stage f_{t-1}, zero the scatter window
+    // ---- 2. stage f_{t-1}, zero the scatter window
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
         const int i = threadIdx.x + it * NT;
@@ -150,162 +253,198 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
 #pragma unroll
     for (int it = 0; it < CIT; ++it) {
         const int i = threadIdx.x + it * NT;
-        if (i < NC) gwin[i] = 0.f;
+        if (i < NC) gacc[i] = 0ull;
     }
     lds_barrier();
 
-    if (active) {
-        // ---- dL/dp_t from the next step's scatter (f_t = p_t * conf') and the direct grads
-        float g = has_conf ? gfr[0] * ce[0] : gfr[0];
-        if (a.g_inter) g += gi[0];
-        if (a.last && a.g_pred) g += clip ? gpr[0] : (pt[0] >= 0.f ? gpr[0] : 0.f);  // pred = clamp(p_T, 0)
-        if (has_conf) {
-            const rsrc_t rgc = make_rsrc(a.g_conf + b * HW);
-            float gc[1];
-            BVec<float, 1>::load(rgc, vpix, 0u, gc);
-            gc[0] += gfr[0] * pt[0];
-            BVec<float, 1>::store(rgc, vpix, 0u, gc);
-        }
-        const float zero[1] = {0.f};
-        BVec<float, 1>::store(make_rsrc(a.gf_read + b * HW), vpix, 0u, zero);  // consumed: ready for reuse
-
-        // ---- forward recompute of the taps (values, corners) for the clamp mask and grads
-        const float Hf = (float)H, Wf = (float)W;
-        float val[K], asum = 0.f;
-        bool valid[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int t = k < REF ? k : k + 1;
-            const int i = t / KW, j = t % KW;
-            asum += av[k][0];
-            float hs, ws;
-            if (OFFSET) {
-                hs = (float)(y - PH + i) + dh[k][0];
-                ws = (float)(x - PW + j) + dw[k][0];
-            } else {
-                int yy = y + i - 1, xx = x + j - 1;
-                yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
-                xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
-                hs = (float)yy;
-                ws = (float)xx;
-            }
-            valid[k] = hs > -1.f && ws > -1.f && hs < Hf && ws < Wf;
-            float v = 0.f;
-            if (valid[k]) {
-                const int hl = (int)floorf(hs), wl = (int)floorf(ws);
-                const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
-                float v1, v2, v3, v4;
-                const int ry = hl - wy0, rx = wl - wx0;
-                if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
-                    const float *s = &win[ry * WW + rx];
-                    v1 = s[0]; v2 = s[1]; v3 = s[WW]; v4 = s[WW + 1];
-                } else {
-                    const int r0 = hl * W, r1 = (hl + 1) * W;
-                    v1 = (hl >= 0 && wl >= 0) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + wl) * ES) : 0.f;
-                    v2 = (hl >= 0 && wl + 1 <= W - 1) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r0 + wl + 1) * ES) : 0.f;
-                    v3 = (hl + 1 <= H - 1 && wl >= 0) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + wl) * ES) : 0.f;
-                    v4 = (hl + 1 <= H - 1 && wl + 1 <= W - 1) ? fetch_f<float, FIRST>(rp, rc, rd, has_conf, preserve, clip, (r1 + wl + 1) * ES) : 0.f;
-                }
-                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                v = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
-                // coordinate weights, mdmcn_get_coordinate_weight (.cuh:84-125); corners
-                // outside the image are zero in the window / fetch, as the checks there
-                if (OFFSET) {
-                    float cwh = 0.f, cww = 0.f;
-                    cwh += -1 * hw * v1;
-                    cwh += -1 * lw * v2;
-                    cwh += hw * v3;
-                    cwh += lw * v4;
-                    cww += -1 * hh * v1;
-                    cww += hh * v2;
-                    cww += -1 * lh * v3;
-                    cww += lh * v4;
-                    dh[k][0] = cwh;  // reuse the offset registers for the coordinate weights
-                    dw[k][0] = cww;
-                }
-            }
-            val[k] = v;
-        }
-        const float fown = win[(ly + RY) * WW + lx + RX];
-        const float aref = 1.0f - asum;
-        if (clip) {
-            float acc = 0.f;
-#pragma unroll
-            for (int t = 0; t < KK; ++t) acc += t == REF ? fown * aref : val[t < REF ? t : t - 1] * av[t < REF ? t : t - 1][0];
-            float pre = acc;
-            if (preserve) {
-                const float m = dv[0] > 0.f ? 1.f : 0.f;
-                pre = (1.0f - m) * acc + m * dv[0];
-            }
-            if (!(pre >= 0.f)) g = 0.f;  // clamp(min=0) passes the gradient where x >= 0
-        }
-        const float go = preserve ? (1.0f - (dv[0] > 0.f ? 1.f : 0.f)) * g : g;
-
-        // ---- per-pixel accumulators: dL/d(aff) (K+1 planes), dL/d(offset) (2K planes)
-        const rsrc_t rga = make_rsrc(a.g_aff + b * (K + 1) * HW);
-        const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * 2 * K * HW : a.g_aff);
-#pragma unroll
-        for (int c = 0; c < K + 1; ++c) {
-            float ga[1];
-            BVec<float, 1>::load(rga, vpix, (unsigned)c * plane_bytes, ga);
-            ga[0] += go * (c == REF ? fown : val[c < REF ? c : c - 1]);
-            BVec<float, 1>::store(rga, vpix, (unsigned)c * plane_bytes, ga);
-        }
+    // ---- per pixel: dL/dp_t (the next step's scatter through f_t = p_t * conf', plus
+    //      direct grads), the clamp mask, dL/dout = go
+    const float Hf = (float)H, Wf = (float)W;
+    auto tap_pos = [&](int k, float &hs, float &ws) {
+        const int t = k < REF ? k : k + 1;
+        const int i = t / KW, j = t % KW;
         if (OFFSET) {
+            hs = (float)(y - PH + i) + dh[k];
+            ws = (float)(x - PW + j) + dw[k];
+        } else {
+            int yy = y + i - 1, xx = x + j - 1;
+            yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+            xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+            hs = (float)yy;
+            ws = (float)xx;
+        }
+    };
+    const float fown = win[(ly + RY) * WW + lx + RX];
+    float asum = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) asum += av[k];
+    const float aref = 1.0f - asum;
+    float go = 0.f, mass = 0.f;
+    if (active) {
+        float g = has_conf ? gfr * ce : gfr;
+        if (a.g_inter) g += gi;
+        if (last && a.g_pred) g += clip ? gpr : (pt >= 0.f ? gpr : 0.f);  // pred = clamp(p_T, 0)
+        if (has_conf) bst(rgc, vpix, 0u, gcv + gfr * pt);
+        bst(rgf, vpix, 0u, 0.f);  // consumed: ready for reuse as a scatter target
+        if (clip) {
+            // recompute the forward value for the clamp mask (torch clamp passes the gradient where x >= 0)
+            float val[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                if (!valid[k]) continue;
-                float g2[1], g3[1];
-                BVec<float, 1>::load(rgo, vpix, (2u * k) * plane_bytes, g2);
-                BVec<float, 1>::load(rgo, vpix, (2u * k + 1) * plane_bytes, g3);
-                g2[0] += dh[k][0] * go * av[k][0];
-                g3[0] += dw[k][0] * go * av[k][0];
-                BVec<float, 1>::store(rgo, vpix, (2u * k) * plane_bytes, g2);
-                BVec<float, 1>::store(rgo, vpix, (2u * k + 1) * plane_bytes, g3);
+                float hs, ws;
+                tap_pos(k, hs, ws);
+                val[k] = 0.f;
+                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                    int hl, wl;
+                    float v[4];
+                    tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf, preserve, clip, hl, wl, v);
+                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                    val[k] = (hh * hw * v[0] + hh * lw * v[1] + lh * hw * v[2] + lh * lw * v[3]);
+                }
             }
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < KK; ++t) acc += t == REF ? fown * aref : val[t < REF ? t : t - 1] * av[t < REF ? t : t - 1];
+            float pre = acc;
+            if (preserve) {
+                const float m = dv > 0.f ? 1.f : 0.f;
+                pre = (1.0f - m) * acc + m * dv;
+            }
+            if (!(pre >= 0.f)) g = 0.f;
         }
+        go = preserve ? (1.0f - (dv > 0.f ? 1.f : 0.f)) * g : g;
+        // bound on everything this pixel scatters: |go| (|a_ref| + sum |a_k|), bilinear weights <= 1
+        float as = fabsf(aref);
+#pragma unroll
+        for (int k = 0; k < K; ++k) as += fabsf(av[k]);
+        mass = fabsf(go) * as;
+    }
 
-        // ---- scatter dL/df_{t-1} (col2im): LDS window, global atomics outside it
+    // ---- the tile's scatter scale.  dL/df_{t-1} is accumulated in LDS as 64-bit
+    // fixed point (ds_add_u64: integer LDS atomics run at ~3x the rate of ds_add_f32
+    // on gfx950, tools/bwd_bench), scaled by 2^sh so the tile's total scattered mass
+    // stays below 2^59: every float contribution converts exactly up to a rounding
+    // of 2^-sh (~2^-59 of the tile's mass), and the window sums are exact, so they do
+    // not depend on arrival order.  Non-finite mass: plain float global atomics.
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mass += __shfl_xor(mass, o, 64);
+    if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = mass;
+    lds_barrier();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) tot += redm[i];
+    const bool exact = tot < 3.0e38f;  // finite (NaN compares false); 0 scatters nothing
+    const int sh = exact && tot > 0.f ? 58 - ilogbf(tot) : 0;
+
+    float gsum = 0.f;
+    if (active) {
+        // ---- taps: dL/daff (G form), dL/doffset (coordinate weights, .cuh:84-125),
+        //      and the col2im scatter of dL/df_{t-1} (.cuh:196-254)
         float *gfw = a.gf_write + b * HW;
-        atomicAdd(&gwin[(ly + RY) * WW + lx + RX], go * aref);  // reference tap, weight (1,0,0,0)
+        auto add_win = [&](int cell, float v) {
+            atomicAdd(&gacc[cell], (unsigned long long)__float2ll_rn(ldexpf(v, sh)));
+        };
+        if (exact) add_win((ly + RY) * WW + lx + RX, go * aref);  // reference tap: integer point, weight 1
+        else atomicAdd(&gfw[y * W + x], go * aref);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            if (!valid[k]) continue;
-            const int t = k < REF ? k : k + 1;
-            const int i = t / KW, j = t % KW;
             float hs, ws;
-            if (OFFSET) {
-                // recompute the sample point from the raw offsets (dh/dw now hold coordinate weights)
-                float o1[1], o2[1];
-                BVec<float, 1>::load(ro, vpix, (2u * k) * plane_bytes, o1);
-                BVec<float, 1>::load(ro, vpix, (2u * k + 1) * plane_bytes, o2);
-                hs = (float)(y - PH + i) + o1[0];
-                ws = (float)(x - PW + j) + o2[0];
-            } else {
-                int yy = y + i - 1, xx = x + j - 1;
-                yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
-                xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
-                hs = (float)yy;
-                ws = (float)xx;
-            }
-            const float top = go * av[k][0];
-            const int hl = (int)floorf(hs), wl = (int)floorf(ws);
-            const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
-            const float wts[4] = {hh * hw, hh * lw, lh * hw, lh * lw};
-            const int ry = hl - wy0, rx = wl - wx0;
-            const bool inwin = (unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1);
+            tap_pos(k, hs, ws);
+            float val = 0.f;
+            if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                int hl, wl;
+                float v[4];
+                const bool inwin = tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf,
+                                                              preserve, clip, hl, wl, v);
+                const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
+                const float top = go * av[k];
+                if (OFFSET) {
+                    float cwh = 0.f, cww = 0.f;
+                    cwh += -1 * hw * v[0];
+                    cwh += -1 * lw * v[1];
+                    cwh += hw * v[2];
+                    cwh += lw * v[3];
+                    cww += -1 * hh * v[0];
+                    cww += hh * v[1];
+                    cww += -1 * lh * v[2];
+                    cww += lh * v[3];
+                    cO[2 * k] += cwh * go * av[k];
+                    cO[2 * k + 1] += cww * go * av[k];
+                }
+                if (inwin && exact) {
+                    // out-of-image cells of the window are dropped by the flush (as the reference's checks)
+                    const int c0 = (hl - wy0) * WW + (wl - wx0);
+                    add_win(c0, w1 * top);
+                    add_win(c0 + 1, w2 * top);
+                    add_win(c0 + WW, w3 * top);
+                    add_win(c0 + WW + 1, w4 * top);
+                } else {
+                    const float wts[4] = {w1, w2, w3, w4};
 #pragma unroll
-            for (int cnr = 0; cnr < 4; ++cnr) {
-                const int hy = hl + (cnr >> 1), wx = wl + (cnr & 1);
-                if (hy < 0 || hy > H - 1 || wx < 0 || wx > W - 1) continue;
-                const float v = wts[cnr] * top;
-                if (inwin) atomicAdd(&gwin[(ry + (cnr >> 1)) * WW + rx + (cnr & 1)], v);
-                else atomicAdd(&gfw[hy * W + wx], v);
+                    for (int cnr = 0; cnr < 4; ++cnr) {
+                        const int hy = hl + (cnr >> 1), wx = wl + (cnr & 1);
+                        if (hy >= 0 && hy <= H - 1 && wx >= 0 && wx <= W - 1) atomicAdd(&gfw[hy * W + wx], wts[cnr] * top);
+                    }
+                }
+            }
+            cG[k] += go * (val - fown);
+        }
+
+        // ---- accumulators
+        if (!HOIST && !last) {
+#pragma unroll
+            for (int c0 = 0; c0 < K; c0 += 8) {
+                float t8[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) t8[i] = c0 + i < K ? bld(rga, vpix, (unsigned)(c0 + i) * plane_bytes) : 0.f;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) if (c0 + i < K) cG[c0 + i] = t8[i] + cG[c0 + i];
+            }
+            if (OFFSET) {
+#pragma unroll
+                for (int c0 = 0; c0 < KO; c0 += 8) {
+                    float t8[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) t8[i] = c0 + i < KO ? bld(rgo, vpix, (unsigned)(c0 + i) * plane_bytes) : 0.f;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) if (c0 + i < KO) cO[c0 + i] = t8[i] + cO[c0 + i];
+                }
             }
         }
+        if (OFFSET && !(DIAG & 4)) {
+#pragma unroll
+            for (int k = 0; k < KO; ++k) bst(rgo, vpix, (unsigned)k * plane_bytes, cO[k]);
+        }
+        if (FIRST) {
+            // G is final for this pixel: normalisation backward -> grad_aff_raw, dL/dgamma partial
+            const rsrc_t rar = make_rsrc(a.aff_raw + b * a.aff_raw_bs);
+            float ar[K], ga[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) ar[k] = bld(rar, vpix, (unsigned)k * plane_bytes);
+            gsum = aff_norm_backward<K>(cG, ar, *a.gamma, a.kind, ga);
+            const rsrc_t rout = make_rsrc(a.grad_aff_raw + b * K * HW);
+#pragma unroll
+            for (int k = 0; k < K; ++k) bst(rout, vpix, (unsigned)k * plane_bytes, ga[k]);
+        } else if (!(DIAG & 4)) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) bst(rga, vpix, (unsigned)k * plane_bytes, cG[k]);
+        }
+    }
+    if (FIRST && a.gamma_part) {
+        for (int o = 32; o > 0; o >>= 1) gsum += __shfl_down(gsum, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = gsum;
     }
     lds_barrier();
-    // ---- flush the scatter window (in-image, non-zero cells) with global atomics
+    if (FIRST && a.gamma_part && threadIdx.x == 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) s += red[i];
+        a.gamma_part[blockIdx.x] = s;
+    }
+    // ---- flush the scatter window (in-image, non-zero cells) with global float atomics
+    if ((DIAG & 1) || !exact) return;
     float *gfw = a.gf_write + b * HW;
 #pragma unroll
     for (int it = 0; it < CIT; ++it) {
@@ -313,86 +452,44 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
         if (i < NC) {
             const int r = i / WW, c = i - r * WW;
             const int gy = wy0 + r, gx = wx0 + c;
-            const float v = gwin[i];
-            if (v != 0.f && gy >= 0 && gy < H && gx >= 0 && gx < W) atomicAdd(&gfw[gy * W + gx], v);
+            const long long q = (long long)gacc[i];
+            if (q != 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) atomicAdd(&gfw[gy * W + gx], ldexpf((float)q, -sh));
         }
     }
 }
 
-// Finishing pass: p_0 / conf' / affinity-normalisation backward.
-//   f_0 = p_0 * conf', p_0 = clamp(blend(pred_init)) (nlspnmodel.py:341-348, :351)
-//   conf' = (1-m) conf + m (:333-334)
-//   aff_ref = 1 - sum(aff) (_aff_insert :262-263); _affinity_normalization (:179-201):
-//   u = tanh(a)/(gamma+1e-8) [TGASS] | tanh(a)/gamma [TC] | a [AS/ASS];
-//   s = sum|u| + 1e-4, s = 1 where s < 1 [ASS/TGASS; no gradient there]; aff = u / s [not TC].
-template <int K>
+// Finishing pass (after step 1 has scattered dL/df_0 completely):
+//   f_0 = p_0 * conf', p_0 = clamp(blend(pred_init)) (nlspnmodel.py:341-348, :351),
+//   conf' = (1-m) conf + m (:333-334) -> grad_pred_init, grad_conf;
+// workgroup 0 also sums step 1's per-workgroup dL/dgamma partials in a fixed order.
 __global__ void __launch_bounds__(256) bwd_final_kernel(
-    const float *pred_init, const float *dep, const float *conf, const float *conf_eff, const float *aff_raw,
-    long long aff_bs, const float *gamma_p, const float *gf0, const float *g_aff, const float *g_conf_acc,
-    float *grad_pred_init, float *grad_conf, float *grad_aff_raw, float *grad_gamma, long long HW, int B, int kind,
-    unsigned flags) {
-    constexpr int REF = K / 2;
+    const float *pred_init, const float *dep, const float *conf, const float *conf_eff, const float *gf0,
+    const float *g_conf_acc, float *grad_pred_init, float *grad_conf, long long N, unsigned flags,
+    const float *gamma_part, int n_part, float *grad_gamma) {
     const bool preserve = (flags & kPreserve) != 0, clip = (flags & kAlwaysClip) != 0;
-    const float gamma = *gamma_p;
-    const long long N = (long long)B * HW;
-    float gsum = 0.f;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
-        const long long b = i / HW, q = i - b * HW;
         const float d = preserve ? dep[i] : 0.f;
         const float m = d > 0.f ? 1.f : 0.f;
         float pre = pred_init[i];
         if (preserve) pre = (1.0f - m) * pre + m * d;
         const float p0 = clip ? clamp0(pre) : pre;
-        float g = conf ? gf0[i] * conf_eff[i] : gf0[i];
+        const float gfi = gf0[i];
+        float g = conf ? gfi * conf_eff[i] : gfi;
         if (clip && !(pre >= 0.f)) g = 0.f;
         grad_pred_init[i] = preserve ? (1.0f - m) * g : g;
         if (conf) {
-            const float gc = g_conf_acc[i] + gf0[i] * p0;
+            const float gc = g_conf_acc[i] + gfi * p0;
             grad_conf[i] = preserve ? (1.0f - m) * gc : gc;
         }
-        // aff: G_k = g_aff[k] - g_aff[ref]; normalisation backward
-        const float gref = g_aff[(b * (K + 1) + REF) * HW + q];
-        float u[K], th[K], G[K], s = 0.f, dot = 0.f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float av = aff_raw[b * aff_bs + k * HW + q];
-            th[k] = tanhf(av);
-            u[k] = kind == kAffTC ? th[k] / gamma : (kind == kAffTGASS ? th[k] / (gamma + 1e-8f) : av);
-            s += fabsf(u[k]);
-            G[k] = g_aff[(b * (K + 1) + (k < REF ? k : k + 1)) * HW + q] - gref;
-        }
-        s = s + 1e-4f;
-        const bool clamped = (kind == kAffASS || kind == kAffTGASS) && s < 1.0f;
-        const float se = clamped ? 1.0f : s;
-#pragma unroll
-        for (int k = 0; k < K; ++k) dot += G[k] * u[k];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float gu;
-            if (kind == kAffTC) {
-                gu = G[k];
-            } else {
-                gu = G[k] / se;
-                if (!clamped) {
-                    const float sg = u[k] > 0.f ? 1.f : (u[k] < 0.f ? -1.f : 0.f);
-                    gu += -dot / (se * se) * sg;
-                }
-            }
-            float ga = gu;
-            if (kind == kAffTC) {
-                ga = gu * (1.f - th[k] * th[k]) / gamma;
-            } else if (kind == kAffTGASS) {
-                const float dd = gamma + 1e-8f;
-                ga = gu * (1.f - th[k] * th[k]) / dd;
-                gsum += -gu * th[k] / (dd * dd);
-            }
-            grad_aff_raw[(b * K + k) * HW + q] = ga;
-        }
     }
-    if (grad_gamma && kind == kAffTGASS) {
-        // wave reduction, then one atomic per wave
-        for (int off = 32; off > 0; off >>= 1) gsum += __shfl_down(gsum, off, 64);
-        if ((threadIdx.x & 63) == 0) atomicAdd(grad_gamma, gsum);
+    if (grad_gamma && blockIdx.x == 0) {
+        __shared__ float red[4];
+        float s = 0.f;
+        for (int i = threadIdx.x; i < n_part; i += 256) s += gamma_part[i];
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) *grad_gamma = red[0] + red[1] + red[2] + red[3];
     }
 }
 

@@ -168,8 +168,15 @@ struct BwdLaunch {
     dim3 grid, block;
 };
 
+constexpr int kBwdTH = 8, kBwdTW = 32;  // backward tile (every geometry)
+
+long long bwd_tiles(int B, int H, int W) {
+    return (long long)B * ((H + kBwdTH - 1) / kBwdTH) * ((W + kBwdTW - 1) / kBwdTW);
+}
+
 template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET>
 BwdLaunch make_bwd(BwdArgs &a, bool first) {
+    static_assert(TH == kBwdTH && TW == kBwdTW, "bwd_tiles() sizes the dL/dgamma partials");
     BwdLaunch L;
     L.fn = first ? reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, true>)
                  : reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, false>);
@@ -197,18 +204,6 @@ int select_bwd(BwdArgs &a, int kh, int kw, bool offset, bool vec, bool first, Bw
         return fail(NLSPN_EUNSUPPORTED, "no backward instantiation for a %dx%d geometry (supported: 3x3, 5x5, 1x17)",
                     kh, kw);
     return NLSPN_OK;
-}
-
-template <int K>
-const void *bwd_final_fn() { return reinterpret_cast<const void *>(&bwd_final_kernel<K>); }
-
-const void *select_bwd_final(int K) {
-    switch (K) {
-        case 8: return bwd_final_fn<8>();
-        case 16: return bwd_final_fn<16>();
-        case 24: return bwd_final_fn<24>();
-        default: return nullptr;
-    }
 }
 
 unsigned elementwise_grid(long long groups) {
@@ -444,8 +439,10 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
 }
 
 size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw) {
+    if (B < 1 || H < 1 || W < 1 || kh < 1 || kw < 1) return 0;
     const size_t N = (size_t)B * H * W, K = (size_t)kh * kw - 1;
-    return sizeof(float) * N * (2 + (K + 1) + 1);  // dL/df ping-pong, dL/daff (K+1 planes), dL/dconf'
+    // dL/df ping-pong, G = dL/daff - dL/daff_ref (K planes), dL/dconf', dL/dgamma partials
+    return sizeof(float) * (N * (2 + K + 1) + (size_t)bwd_tiles(B, H, W));
 }
 
 int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -471,16 +468,20 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
     if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
     if (HW * (3LL * K + 4) * 4 > 0x7fffffffLL) return fail(NLSPN_EINVAL, "image too large for one batch item");
-    const void *ffn = select_bwd_final(K);
-    if (!ffn) return fail(NLSPN_EUNSUPPORTED, "no backward for K=%d (supported 8, 16, 24)", K);
     hipStream_t s = as_stream(stream);
     float *ws = static_cast<float *>(workspace);
     float *gf[2] = {ws, ws + N};
     float *g_aff = ws + 2 * N;
-    float *g_conf = ws + (2 + K + 1) * N;
-    NLSPN_HIP_TRY(hipMemsetAsync(workspace, 0, nlspn_backward_workspace_bytes(B, H, W, kh, kw), s));
-    if (off_raw) NLSPN_HIP_TRY(hipMemsetAsync(grad_off_raw, 0, sizeof(float) * 2 * K * N, s));
-    if (grad_gamma) NLSPN_HIP_TRY(hipMemsetAsync(grad_gamma, 0, sizeof(float), s));
+    float *g_conf = ws + (2 + K) * N;
+    float *gpart = ws + (3 + K) * N;
+    {
+        BwdArgs probe{};
+        probe.B = B; probe.H = H; probe.W = W;
+        BwdLaunch L;
+        if (int rc = select_bwd(probe, kh, kw, off_raw != nullptr, false, true, L)) return rc;
+    }
+    // accumulators are initialised by step T; only step T's scatter target needs clearing
+    NLSPN_HIP_TRY(hipMemsetAsync(gf[(T - 1) & 1], 0, sizeof(float) * N, s));
     const bool vec = (W % 4 == 0) && aligned(pred_init, 16) && aligned(pred_inter, 16) && aligned(conf, 16) &&
                      aligned(conf_eff, 16) && aligned(dep, 16);
     const float *pi = static_cast<const float *>(pred_inter);
@@ -506,6 +507,14 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         a.B = B; a.H = H; a.W = W;
         a.last = t == T;
         a.flags = flags;
+        if (first) {
+            a.aff_raw = static_cast<const float *>(aff_raw);
+            a.aff_raw_bs = aff_bstride;
+            a.gamma = gamma;
+            a.grad_aff_raw = static_cast<float *>(grad_aff_raw);
+            a.gamma_part = (grad_gamma && kind == NLSPN_AFF_TGASS) ? gpart : nullptr;
+            a.kind = kind;
+        }
         BwdLaunch L;
         if ((rc = select_bwd(a, kh, kw, off_raw != nullptr, vec, first, L))) return rc;
         void *args[] = {&a};
@@ -513,17 +522,17 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         if ((rc = check_launch("nlspn_propagate_backward step"))) return rc;
     }
     const float *pinit = static_cast<const float *>(pred_init), *pdep = static_cast<const float *>(dep),
-                *pconf = static_cast<const float *>(conf), *pce = static_cast<const float *>(conf_eff),
-                *praw = static_cast<const float *>(aff_raw), *gf0 = gf[0];
-    const float *cg_aff = g_aff, *cg_conf = g_conf;
-    float *gpi = static_cast<float *>(grad_pred_init), *gc = static_cast<float *>(grad_conf),
-          *gar = static_cast<float *>(grad_aff_raw);
-    long long abs_ = aff_bstride, hw = HW;
-    int b_ = B, k_ = kind;
+                *pconf = static_cast<const float *>(conf), *pce = static_cast<const float *>(conf_eff), *gf0 = gf[0];
+    const float *cg_conf = g_conf, *cgpart = gpart;
+    float *gpi = static_cast<float *>(grad_pred_init), *gc = static_cast<float *>(grad_conf);
+    float *gg = (grad_gamma && kind == NLSPN_AFF_TGASS) ? grad_gamma : nullptr;
+    if (grad_gamma && !gg) NLSPN_HIP_TRY(hipMemsetAsync(grad_gamma, 0, sizeof(float), s));
+    long long n_ = N;
+    int np = (int)bwd_tiles(B, H, W);
     unsigned fl = flags;
-    void *fargs[] = {&pinit, &pdep, &pconf, &pce, &praw, &abs_, (void *)&gamma, &gf0, &cg_aff, &cg_conf,
-                     &gpi, &gc, &gar, &grad_gamma, &hw, &b_, &k_, &fl};
-    NLSPN_HIP_TRY(hipLaunchKernel(ffn, dim3(elementwise_grid(N)), dim3(256), fargs, 0, s));
+    void *fargs[] = {&pinit, &pdep, &pconf, &pce, &gf0, &cg_conf, &gpi, &gc, &n_, &fl, &cgpart, &np, &gg};
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&bwd_final_kernel), dim3(elementwise_grid(N)),
+                                  dim3(256), fargs, 0, s));
     return check_launch("nlspn_propagate_backward final");
 }
 

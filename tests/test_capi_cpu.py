@@ -30,6 +30,11 @@ def test_abi_version_and_workspace():
     lib = _lib.get()
     assert lib.nlspn_abi_version() == 1
     assert lib.nlspn_workspace_bytes(0, 8, 228, 304) == 0  # prologue fused into step 1
+    # backward: dL/df ping-pong + K planes of G + dL/dconf' + one dL/dgamma partial per 8x32 tile
+    B, H, W, K = 8, 228, 304, 8
+    tiles = B * ((H + 7) // 8) * ((W + 31) // 32)
+    assert lib.nlspn_backward_workspace_bytes(B, H, W, 3, 3) == 4 * (B * H * W * (3 + K) + tiles)
+    assert lib.nlspn_backward_workspace_bytes(0, H, W, 3, 3) == 0
 
 
 def _call_step(**over):
