@@ -164,6 +164,39 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
                              unsigned flags, void *stream);
 
 /*
+ * Backward of nlspn_prop_step (float32, raw offsets or the no-offset branch): what
+ * autograd computes through one loop iteration, src/model/nlspnmodel.py:350-361, with
+ * the DCNv2 backward of its _propagate_once (modulated_deform_conv_cuda.cu:124-280).
+ * Used by the ConvGRU mode, where every iteration has its own affinity (:365-373).
+ * Inputs are the step's inputs (feat, conf, dep, aff with (K+1) planes, raw offsets)
+ * and grad_out = dL/d(step output).  Writes grad_feat and grad_conf (iff conf),
+ * grad_aff ((K+1) planes per item, contiguous; plane K/2 is 0 because the step
+ * recomputes that tap as 1 - sum of the others, so chaining it into
+ * nlspn_affinity_normalize_backward gives the reference's _aff_insert gradient) and
+ * grad_off (2K planes per item, contiguous).  workspace:
+ * nlspn_prop_step_backward_workspace_bytes() bytes.
+ */
+size_t nlspn_prop_step_backward_workspace_bytes(int B, int H, int W);
+int nlspn_prop_step_backward(int dtype, const void *feat, const void *conf, const void *dep,
+                             const void *aff, int64_t aff_bstride, const void *off_raw,
+                             int64_t off_bstride, const void *grad_out, void *grad_feat,
+                             void *grad_conf, void *grad_aff, void *grad_off, void *workspace,
+                             int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
+
+/*
+ * Backward of nlspn_affinity_normalize (_affinity_normalization + _aff_insert,
+ * src/model/nlspnmodel.py:179-201, :261-269): grad_aff is dL/d(output), (K+1) planes
+ * per item, contiguous; writes grad_aff_raw (K planes per item, contiguous) and, for
+ * TGASS, grad_gamma (1 float, summed in a fixed order; 0 for other kinds; may be
+ * NULL).  workspace: nlspn_affinity_normalize_backward_workspace_bytes() bytes.
+ */
+size_t nlspn_affinity_normalize_backward_workspace_bytes(int B, int K, int H, int W);
+int nlspn_affinity_normalize_backward(int dtype, const void *aff_raw, int64_t aff_bstride,
+                                      const float *gamma, const void *grad_aff, void *grad_aff_raw,
+                                      float *grad_gamma, void *workspace, int B, int K, int H,
+                                      int W, int kind, void *stream);
+
+/*
  * Modulated DCNv2 forward, seam 2 of the drop-in (the `DCN` pybind module,
  * src/model/deformconv/src/vision.cpp:9, modulated_deform_conv.h:10-44,
  * cuda/modulated_deform_conv_cuda.cu:19-121), as one direct (GEMM-free) gather

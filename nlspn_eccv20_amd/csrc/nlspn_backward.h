@@ -48,6 +48,8 @@ struct BwdArgs {
     long long off_bs;
     int B, H, W, tiles_x, tiles_y;
     int last;               // t == T: accumulators are initialised, not read
+    int g_aff_ins;          // 1: g_aff has the inserted (K+1)-plane layout (step-level backward; tap
+                            //    K/2 untouched), 0: K planes (G form)
     unsigned flags;
     // FIRST only: affinity-normalisation backward fused in (per pixel, G final)
     const float *aff_raw;   // raw head affinity, K planes per item at aff_raw_bs
@@ -223,11 +225,13 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     if (has_conf && !last) gcv = bld(rgc, vpix, 0u);
     if (a.g_inter) gi = bld(make_rsrc(a.g_inter + b * HW), vpix, 0u);
     if (last && a.g_pred) gpr = bld(make_rsrc(a.g_pred + b * HW), vpix, 0u);
-    const rsrc_t rga = make_rsrc(a.g_aff + b * K * HW);
+    const bool gins = a.g_aff_ins != 0;
+    const rsrc_t rga = make_rsrc(a.g_aff + b * (gins ? K + 1 : K) * HW);
+    auto gplane = [&](int k) { return (unsigned)(gins && k >= REF ? k + 1 : k) * plane_bytes; };
     const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * 2 * K * HW : a.g_aff);
     float cG[K], cO[KO];
 #pragma unroll
-    for (int k = 0; k < K; ++k) cG[k] = (HOIST && !last && !(DIAG & 4)) ? bld(rga, vpix, (unsigned)k * plane_bytes) : 0.f;
+    for (int k = 0; k < K; ++k) cG[k] = (HOIST && !last && !(DIAG & 4)) ? bld(rga, vpix, gplane(k)) : 0.f;
 #pragma unroll
     for (int k = 0; k < KO; ++k) cO[k] = (OFFSET && HOIST && !last && !(DIAG & 4)) ? bld(rgo, vpix, (unsigned)k * plane_bytes) : 0.f;
 
@@ -398,7 +402,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             for (int c0 = 0; c0 < K; c0 += 8) {
                 float t8[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) t8[i] = c0 + i < K ? bld(rga, vpix, (unsigned)(c0 + i) * plane_bytes) : 0.f;
+                for (int i = 0; i < 8; ++i) t8[i] = c0 + i < K ? bld(rga, vpix, gplane(c0 + i)) : 0.f;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) if (c0 + i < K) cG[c0 + i] = t8[i] + cG[c0 + i];
             }
@@ -429,7 +433,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             for (int k = 0; k < K; ++k) bst(rout, vpix, (unsigned)k * plane_bytes, ga[k]);
         } else if (!(DIAG & 4)) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) bst(rga, vpix, (unsigned)k * plane_bytes, cG[k]);
+            for (int k = 0; k < K; ++k) bst(rga, vpix, gplane(k), cG[k]);
         }
     }
     if (FIRST && a.gamma_part) {
@@ -491,6 +495,68 @@ __global__ void __launch_bounds__(256) bwd_final_kernel(
         __syncthreads();
         if (threadIdx.x == 0) *grad_gamma = red[0] + red[1] + red[2] + red[3];
     }
+}
+
+// Step-level backward, after bwd_step_kernel has scattered dL/df (f = feat * conf) for
+// one prop_step (nlspnmodel.py:350-361): grad_feat = dL/df * conf, grad_conf =
+// dL/df * feat, and tap K/2 of the (K+1)-plane affinity gradient = 0 (the kernels
+// recompute that tap as 1 - sum of the others, so it does not enter the output).
+__global__ void __launch_bounds__(256) bwd_step_io_kernel(const float *feat, const float *conf, const float *gf,
+                                                           float *grad_feat, float *grad_conf, float *grad_aff,
+                                                           long long HW, int B, int K) {
+    const long long N = (long long)B * HW;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
+        const float g = gf[i];
+        grad_feat[i] = conf ? g * conf[i] : g;
+        if (conf) grad_conf[i] = g * feat[i];
+        const long long b = i / HW, q = i - b * HW;
+        grad_aff[(b * (K + 1) + K / 2) * HW + q] = 0.f;
+    }
+}
+
+// Backward of nlspn_affinity_normalize (_affinity_normalization + _aff_insert,
+// nlspnmodel.py:179-201, :261-269) for a (K+1)-plane gradient of its output:
+// G_k = g[k] - g[K/2], then aff_norm_backward; one dL/dgamma partial per workgroup.
+template <int K>
+__global__ void __launch_bounds__(256) affnorm_bwd_kernel(const float *aff_raw, long long aff_bs, const float *gamma_p,
+                                                          const float *grad_aff, float *grad_aff_raw,
+                                                          float *gamma_part, long long HW, int B, int kind) {
+    constexpr int REF = K / 2;
+    const float gamma = *gamma_p;
+    const long long N = (long long)B * HW;
+    float gsum = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
+        const long long b = i / HW, q = i - b * HW;
+        const float *gin = grad_aff + b * (K + 1) * HW + q;
+        const float gref = gin[REF * HW];
+        float G[K], ar[K], ga[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            G[k] = gin[(k < REF ? k : k + 1) * HW] - gref;
+            ar[k] = aff_raw[b * aff_bs + k * HW + q];
+        }
+        gsum += aff_norm_backward<K>(G, ar, gamma, kind, ga);
+#pragma unroll
+        for (int k = 0; k < K; ++k) grad_aff_raw[(b * K + k) * HW + q] = ga[k];
+    }
+    if (gamma_part) {
+        __shared__ float red[4];
+        for (int o = 32; o > 0; o >>= 1) gsum += __shfl_down(gsum, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = gsum;
+        __syncthreads();
+        if (threadIdx.x == 0) gamma_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    }
+}
+
+// Fixed-order sum of n partials into *out (one workgroup).
+__global__ void __launch_bounds__(256) sum_partials_kernel(const float *part, int n, float *out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
 }
 
 }  // namespace nlspn

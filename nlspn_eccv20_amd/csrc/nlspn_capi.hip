@@ -536,4 +536,110 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     return check_launch("nlspn_propagate_backward final");
 }
 
+size_t nlspn_prop_step_backward_workspace_bytes(int B, int H, int W) {
+    if (B < 1 || H < 1 || W < 1) return 0;
+    return sizeof(float) * 2 * (size_t)B * H * W;  // dL/df, plus a scratch plane
+}
+
+int nlspn_prop_step_backward(int dtype, const void *feat, const void *conf, const void *dep, const void *aff,
+                             int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const void *grad_out,
+                             void *grad_feat, void *grad_conf, void *grad_aff, void *grad_off, void *workspace, int B,
+                             int H, int W, int kh, int kw, unsigned flags, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the backward is implemented for float32 storage");
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
+        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
+    if (!feat || !aff || !grad_out || !grad_feat || !grad_aff || !workspace)
+        return fail(NLSPN_EINVAL, "null required pointer");
+    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    if (conf && !grad_conf) return fail(NLSPN_EINVAL, "conf given without grad_conf");
+    if (off_raw && !grad_off) return fail(NLSPN_EINVAL, "off_raw given without grad_off");
+    const int K = kh * kw - 1;
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    if (aff_bstride < (long long)(K + 1) * HW) return fail(NLSPN_EINVAL, "aff batch stride < (K+1)*H*W");
+    if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
+    if (HW * (3LL * K + 4) * 4 > 0x7fffffffLL) return fail(NLSPN_EINVAL, "image too large for one batch item");
+    hipStream_t s = as_stream(stream);
+    float *ws = static_cast<float *>(workspace);
+    BwdArgs a{};
+    a.p_in = static_cast<const float *>(feat);
+    a.p_out = a.p_in;  // read only for terms that vanish at a single step (no incoming dL/df)
+    a.conf = static_cast<const float *>(conf);
+    a.conf_eff = a.conf;
+    a.dep = static_cast<const float *>(dep);
+    a.aff = static_cast<const float *>(aff);
+    a.off = static_cast<const float *>(off_raw);
+    a.g_inter = static_cast<const float *>(grad_out);
+    a.gf_write = ws;
+    a.gf_read = ws + N;
+    a.g_aff = static_cast<float *>(grad_aff);
+    a.g_aff_ins = 1;
+    a.g_off = static_cast<float *>(grad_off);
+    a.g_conf = conf ? static_cast<float *>(grad_conf) : nullptr;
+    a.off_bs = off_bstride;
+    a.B = B; a.H = H; a.W = W;
+    a.last = 1;
+    a.flags = flags;
+    const bool vec = (W % 4 == 0) && aligned(feat, 16) && aligned(conf, 16) && aligned(dep, 16);
+    BwdLaunch L;
+    if (int rc = select_bwd(a, kh, kw, off_raw != nullptr, vec, false, L)) return rc;
+    NLSPN_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(float) * N, s));
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(L.fn, L.grid, L.block, args, 0, s));
+    if (int rc = check_launch("nlspn_prop_step_backward step")) return rc;
+    const float *pf = a.p_in, *pc = a.conf, *gf = ws;
+    float *gfe = static_cast<float *>(grad_feat), *gc = static_cast<float *>(grad_conf),
+          *ga = static_cast<float *>(grad_aff);
+    long long hw = HW;
+    int b_ = B, k_ = K;
+    void *iargs[] = {&pf, &pc, &gf, &gfe, &gc, &ga, &hw, &b_, &k_};
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&bwd_step_io_kernel), dim3(elementwise_grid(N)),
+                                  dim3(256), iargs, 0, s));
+    return check_launch("nlspn_prop_step_backward io");
+}
+
+size_t nlspn_affinity_normalize_backward_workspace_bytes(int B, int K, int H, int W) {
+    if (B < 1 || K < 1 || H < 1 || W < 1) return 0;
+    return sizeof(float) * elementwise_grid((long long)B * H * W);  // dL/dgamma partials
+}
+
+int nlspn_affinity_normalize_backward(int dtype, const void *aff_raw, int64_t aff_bstride, const float *gamma,
+                                      const void *grad_aff, void *grad_aff_raw, float *grad_gamma, void *workspace,
+                                      int B, int K, int H, int W, int kind, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the backward is implemented for float32 storage");
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    if (!aff_raw || !gamma || !grad_aff || !grad_aff_raw || !workspace) return fail(NLSPN_EINVAL, "null required pointer");
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
+    const void *fn = nullptr;
+    switch (K) {
+        case 8: fn = reinterpret_cast<const void *>(&affnorm_bwd_kernel<8>); break;
+        case 16: fn = reinterpret_cast<const void *>(&affnorm_bwd_kernel<16>); break;
+        case 24: fn = reinterpret_cast<const void *>(&affnorm_bwd_kernel<24>); break;
+        case 48: fn = reinterpret_cast<const void *>(&affnorm_bwd_kernel<48>); break;
+        default: return fail(NLSPN_EUNSUPPORTED, "no affinity-normalisation backward for K=%d (8, 16, 24, 48)", K);
+    }
+    hipStream_t s = as_stream(stream);
+    const unsigned grid = elementwise_grid(N);
+    float *part = (grad_gamma && kind == NLSPN_AFF_TGASS) ? static_cast<float *>(workspace) : nullptr;
+    if (grad_gamma && !part) NLSPN_HIP_TRY(hipMemsetAsync(grad_gamma, 0, sizeof(float), s));
+    const float *ar = static_cast<const float *>(aff_raw), *gin = static_cast<const float *>(grad_aff);
+    float *gout = static_cast<float *>(grad_aff_raw);
+    long long abs_ = aff_bstride, hw = HW;
+    int b_ = B, k_ = kind;
+    void *args[] = {&ar, &abs_, (void *)&gamma, &gin, &gout, &part, &hw, &b_, &k_};
+    NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s));
+    if (int rc = check_launch("nlspn_affinity_normalize_backward")) return rc;
+    if (part) {
+        const float *cp = part;
+        int n = (int)grid;
+        void *rargs[] = {&cp, &n, &grad_gamma};
+        NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&sum_partials_kernel), dim3(1), dim3(256), rargs,
+                                      0, s));
+        return check_launch("nlspn_affinity_normalize_backward gamma");
+    }
+    return NLSPN_OK;
+}
+
 }  // extern "C"

@@ -15,14 +15,15 @@ Propagation: without the ConvGRU the whole section is one fused, differentiable
 op (propagate: prop_time launches).  With use_GRU (the reference's forced default,
 src/config.py:225-228) the affinity is re-estimated after every iteration
 (nlspnmodel.py:365-373), so each iteration is prop_step + affinity_normalization
-around the GRU's MIOpen convolutions; that mode is inference-only this round.
+around the GRU's MIOpen convolutions; both are differentiable (step-level backward
+kernels), so that mode trains too.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
-from .propagation import affinity_normalization, kernel_geometry, prop_step, propagate
+from .propagation import affinity_normalization, kernel_geometry, off_insert, prop_step, propagate
 
 __all__ = ["NLSPNModel", "ConvGRU", "S2D", "conv_bn_relu", "convt_bn_relu", "get_resnet18", "get_resnet34", "get"]
 
@@ -302,30 +303,66 @@ class NLSPNModel(nn.Module):
 
     def _forward_gru(self, pred_init, dep, off, aff_raw, confidence):
         """nlspnmodel.py:323-383 with use_GRU: the affinity is re-estimated after every
-        iteration (:365-373).  Iteration 1 runs the fused first step (prologue inside);
-        later iterations run prop_step on the GRU's freshly normalised affinity."""
+        iteration (:365-373).  Inference: iteration 1 runs the fused first step (prologue
+        inside), later iterations prop_step on the GRU's freshly normalised affinity.
+        With gradients: the prologue in torch, then T differentiable prop_steps
+        (nlspn_prop_step_backward) and differentiable normalisations."""
         a = self.args
-        if torch.is_grad_enabled() and self.training:
-            raise NotImplementedError("GRU-mode propagation is inference-only this round (build plan §8f rank 2)")
-        with torch.no_grad():
-            o = propagate(pred_init, dep if a.preserve_input else None, confidence if a.conf_prop else None,
-                          aff_raw, off, self.aff_scale_const, prop_time=1, affinity=a.affinity,
-                          kernel=(self.kh, self.kw), preserve_input=a.preserve_input, always_clip=a.always_clip)
-            new_pred = o["pred_inter"][0]
-            aff, conf_eff = o["aff"], o["confidence"]
-            list_pred = [new_pred]
-            for k in range(2, a.prop_time + 1):
-                dep_feat = self.encode_dep(new_pred / a.max_depth)
-                if k == 2:
-                    aff_feat = self.encode_aff(aff)
-                aff_feat = self.GRU(h=aff_feat, x=dep_feat)
-                aff = self._aff_head(aff_feat)
-                new_pred = prop_step(new_pred, conf_eff, dep if a.preserve_input else None, aff, off,
-                                     kernel=(self.kh, self.kw), offset_layout="raw", preserve_input=a.preserve_input,
-                                     always_clip=a.always_clip)
-                list_pred.append(new_pred)
-            pred = new_pred if a.always_clip else torch.clamp(new_pred, min=0)
+        if torch.is_grad_enabled():
+            return self._forward_gru_train(pred_init, dep, off, aff_raw, confidence)
+        o = propagate(pred_init, dep if a.preserve_input else None, confidence if a.conf_prop else None,
+                      aff_raw, off, self.aff_scale_const, prop_time=1, affinity=a.affinity,
+                      kernel=(self.kh, self.kw), preserve_input=a.preserve_input, always_clip=a.always_clip)
+        new_pred = o["pred_inter"][0]
+        aff, conf_eff = o["aff"], o["confidence"]
+        list_pred = [new_pred]
+        aff_feat = None
+        for k in range(2, a.prop_time + 1):
+            aff_feat = self._gru_update(aff_feat, aff, new_pred, k)
+            aff = self._aff_head(aff_feat)
+            new_pred = prop_step(new_pred, conf_eff, dep if a.preserve_input else None, aff, off,
+                                 kernel=(self.kh, self.kw), offset_layout="raw", preserve_input=a.preserve_input,
+                                 always_clip=a.always_clip)
+            list_pred.append(new_pred)
+        pred = new_pred if a.always_clip else torch.clamp(new_pred, min=0)
         return {"pred": pred, "pred_init": pred_init, "pred_inter": list_pred, "offset": o["offset"], "aff": aff,
+                "gamma": self.aff_scale_const.data, "confidence": conf_eff}
+
+    def _gru_update(self, aff_feat, aff, new_pred, k):
+        """nlspnmodel.py:365-371: encode the new depth, (at the first update) encode the
+        affinity, one ConvGRU step."""
+        dep_feat = self.encode_dep(new_pred / self.args.max_depth)
+        if k == 2:
+            aff_feat = self.encode_aff(aff)
+        return self.GRU(h=aff_feat, x=dep_feat)
+
+    def _forward_gru_train(self, pred_init, dep, off, aff_raw, confidence):
+        a = self.args
+        kern = (self.kh, self.kw)
+        aff = affinity_normalization(aff_raw, self.aff_scale_const, a.affinity)
+        conf_eff = confidence if a.conf_prop else None
+        new_pred = pred_init
+        if a.preserve_input:  # :328-334, :341-345
+            mask_fix = (dep > 0.0).to(dep.dtype)
+            if conf_eff is not None:
+                conf_eff = (1.0 - mask_fix) * conf_eff + mask_fix
+            new_pred = (1.0 - mask_fix) * new_pred + mask_fix * dep
+        if a.always_clip:
+            new_pred = torch.clamp(new_pred, min=0)
+        new_pred = new_pred.contiguous()
+        conf_eff = None if conf_eff is None else conf_eff.contiguous()
+        list_pred = []
+        aff_feat = None
+        for k in range(1, a.prop_time + 1):
+            if k > 1:
+                aff_feat = self._gru_update(aff_feat, aff, new_pred, k)
+                aff = self._aff_head(aff_feat)
+            new_pred = prop_step(new_pred, conf_eff, dep if a.preserve_input else None, aff, off, kernel=kern,
+                                 offset_layout="raw", preserve_input=a.preserve_input, always_clip=a.always_clip)
+            list_pred.append(new_pred)
+        pred = new_pred if a.always_clip else torch.clamp(new_pred, min=0)
+        offset = off_insert(off) if off is not None else None
+        return {"pred": pred, "pred_init": pred_init, "pred_inter": list_pred, "offset": offset, "aff": aff,
                 "gamma": self.aff_scale_const.data, "confidence": conf_eff}
 
 

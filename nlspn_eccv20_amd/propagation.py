@@ -86,9 +86,7 @@ def _gamma_f32(gamma) -> torch.Tensor:
 
 
 # -------------------------------------------------------------- functional ops
-def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "TGASS") -> torch.Tensor:
-    """NLSPNModel._affinity_normalization + _aff_insert (nlspnmodel.py:179-201, :261-269).
-    aff (B, K, H, W) raw -> (B, K+1, H, W), reference tap at K//2."""
+def _affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str) -> torch.Tensor:
     _cuda("aff", aff)
     if kind not in _lib.AFF_KINDS:
         raise NotImplementedError(kind)
@@ -103,6 +101,47 @@ def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "
     return out
 
 
+class _AffNormFn(torch.autograd.Function):
+    """Autograd node for affinity_normalization; backward = nlspn_affinity_normalize_backward."""
+
+    @staticmethod
+    def forward(ctx, aff, gamma, kind):
+        ctx.kind = kind
+        ctx.save_for_backward(aff, gamma)
+        return _affinity_normalization(aff, gamma, kind)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_out):
+        aff, gamma = ctx.saved_tensors
+        if aff.dtype != torch.float32:
+            raise NotImplementedError("the affinity-normalisation backward is implemented for float32 storage")
+        B, K, H, W = aff.shape
+        f32 = dict(dtype=torch.float32, device=aff.device)
+        g_out = g_out.contiguous()
+        g_raw = torch.empty((B, K, H, W), **f32)
+        want_g = ctx.kind == "TGASS" and ctx.needs_input_grad[1]
+        g_gamma = torch.empty(1, **f32) if want_g else None
+        lib = _lib.get()
+        ws = torch.empty(max(1, lib.nlspn_affinity_normalize_backward_workspace_bytes(B, K, H, W) // 4), **f32)
+        with torch.cuda.device(aff.device):
+            _lib.check(lib.nlspn_affinity_normalize_backward(
+                _lib.DTYPE_F32, _ptr(aff), _planes("aff", aff, B, K, H, W), _ptr(_gamma_f32(gamma)), _ptr(g_out),
+                _ptr(g_raw), _ptr(g_gamma), _ptr(ws), B, K, H, W, _lib.AFF_KINDS[ctx.kind], _stream(aff.device)))
+        if g_gamma is not None:
+            g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype)
+        return g_raw, g_gamma, None
+
+
+def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "TGASS") -> torch.Tensor:
+    """NLSPNModel._affinity_normalization + _aff_insert (nlspnmodel.py:179-201, :261-269).
+    aff (B, K, H, W) raw -> (B, K+1, H, W), reference tap at K//2.  Differentiable
+    (float32) in aff and, for TGASS, gamma."""
+    if torch.is_grad_enabled() and (aff.requires_grad or (torch.is_tensor(gamma) and gamma.requires_grad)):
+        return _AffNormFn.apply(aff, gamma, kind)
+    return _affinity_normalization(aff, gamma, kind)
+
+
 def off_insert(offset: torch.Tensor) -> torch.Tensor:
     """NLSPNModel._off_insert (nlspnmodel.py:252-259): (B, 2K, H, W) -> (B, 2(K+1), H, W)
     with a zero (dh, dw) pair at tap K//2.  A layout conversion, kept in torch."""
@@ -113,17 +152,8 @@ def off_insert(offset: torch.Tensor) -> torch.Tensor:
     return torch.cat([o[:, :K // 2], z, o[:, K // 2:]], 1).reshape(B, -1, H, W)
 
 
-def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optional[torch.Tensor],
-              aff: torch.Tensor, offset: Optional[torch.Tensor] = None, *, kernel=(3, 3),
-              offset_layout: str = "inserted", preserve_input: bool = True, always_clip: bool = False,
-              out: Optional[torch.Tensor] = None, pred_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """One fused iteration (nlspnmodel.py:350-361): out = _propagate_once(feat*confidence,
-    offset, aff), then the preserve-input blend with dep and the optional clamp.
-
-    aff: normalised (B, K+1, H, W) (the output of affinity_normalization; its tap K//2 is
-    recomputed in-kernel as 1 - sum of the others).  offset: (B, 2(K+1), H, W) inserted
-    layout or (B, 2K, H, W) with offset_layout="raw"; None = no-offset branch (3x3 replicate).
-    """
+def _prop_step(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input, always_clip, out=None,
+               pred_out=None):
     kh, kw = kernel_geometry(kernel)
     K = kh * kw - 1
     for n, t in (("feat", feat), ("confidence", confidence), ("dep", dep), ("aff", aff), ("offset", offset)):
@@ -152,6 +182,65 @@ def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optio
             _dtype_code(feat), _ptr(feat), _ptr(confidence), _ptr(dep), _ptr(aff), abs_, _ptr(offset), obs,
             layout, _ptr(out), _ptr(pred_out), B, H, W, kh, kw, flags, _stream(feat.device)))
     return out
+
+
+class _PropStepFn(torch.autograd.Function):
+    """Autograd node for one prop_step; backward = nlspn_prop_step_backward (float32,
+    raw offset layout).  dep receives no gradient (the reference's sparse input)."""
+
+    @staticmethod
+    def forward(ctx, feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input, always_clip):
+        ctx.cfg = (kernel_geometry(kernel), offset_layout, preserve_input, always_clip)
+        ctx.save_for_backward(feat, confidence, dep, aff, offset)
+        return _prop_step(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input, always_clip)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_out):
+        feat, conf, dep, aff, off = ctx.saved_tensors
+        (kh, kw), layout, preserve, clip = ctx.cfg
+        if feat.dtype != torch.float32:
+            raise NotImplementedError("the prop_step backward is implemented for float32 storage")
+        if off is not None and layout != "raw":
+            raise NotImplementedError("the prop_step backward takes offset_layout='raw' (B, 2K, H, W) offsets")
+        B, _, H, W = feat.shape
+        K = kh * kw - 1
+        f32 = dict(dtype=torch.float32, device=feat.device)
+        g_feat = torch.empty((B, 1, H, W), **f32)
+        g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
+        g_aff = torch.empty((B, K + 1, H, W), **f32)
+        g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+        lib = _lib.get()
+        ws = torch.empty(lib.nlspn_prop_step_backward_workspace_bytes(B, H, W) // 4, **f32)
+        flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
+        with torch.cuda.device(feat.device):
+            _lib.check(lib.nlspn_prop_step_backward(
+                _lib.DTYPE_F32, _ptr(feat), _ptr(conf), _ptr(dep), _ptr(aff), _planes("aff", aff, B, K + 1, H, W),
+                _ptr(off), _planes("offset", off, B, 2 * K, H, W) if off is not None else 0,
+                _ptr(g_out.contiguous()), _ptr(g_feat), _ptr(g_conf), _ptr(g_aff), _ptr(g_off), _ptr(ws),
+                B, H, W, kh, kw, flags, _stream(feat.device)))
+        return g_feat, g_conf, None, g_aff, g_off, None, None, None, None
+
+
+def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optional[torch.Tensor],
+              aff: torch.Tensor, offset: Optional[torch.Tensor] = None, *, kernel=(3, 3),
+              offset_layout: str = "inserted", preserve_input: bool = True, always_clip: bool = False,
+              out: Optional[torch.Tensor] = None, pred_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One fused iteration (nlspnmodel.py:350-361): out = _propagate_once(feat*confidence,
+    offset, aff), then the preserve-input blend with dep and the optional clamp.
+
+    aff: normalised (B, K+1, H, W) (the output of affinity_normalization; its tap K//2 is
+    recomputed in-kernel as 1 - sum of the others).  offset: (B, 2(K+1), H, W) inserted
+    layout or (B, 2K, H, W) with offset_layout="raw"; None = no-offset branch (3x3 replicate).
+    Differentiable (float32, raw offsets) in feat, confidence, aff and offset when called
+    without out/pred_out.
+    """
+    if (out is None and pred_out is None and torch.is_grad_enabled()
+            and any(t is not None and t.requires_grad for t in (feat, confidence, aff, offset))):
+        return _PropStepFn.apply(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input,
+                                 always_clip)
+    return _prop_step(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input, always_clip, out,
+                      pred_out)
 
 
 def _alloc_outputs(pred_init, K, T, with_off, with_conf):

@@ -35,6 +35,8 @@ def test_abi_version_and_workspace():
     tiles = B * ((H + 7) // 8) * ((W + 31) // 32)
     assert lib.nlspn_backward_workspace_bytes(B, H, W, 3, 3) == 4 * (B * H * W * (3 + K) + tiles)
     assert lib.nlspn_backward_workspace_bytes(0, H, W, 3, 3) == 0
+    assert lib.nlspn_prop_step_backward_workspace_bytes(B, H, W) == 4 * 2 * B * H * W
+    assert lib.nlspn_affinity_normalize_backward_workspace_bytes(B, K, H, W) > 0
 
 
 def _call_step(**over):

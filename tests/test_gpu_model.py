@@ -139,10 +139,45 @@ def test_model_gru_vs_oracle(oracle, kw):
     assert rel(np32(out["aff"]), aff) <= 1e-4
 
 
-def test_model_gru_training_raises():
-    m = NLSPNModel(make_args(prop_time=2, patch_height=32, patch_width=48)).to(DEV).train()
-    with pytest.raises(NotImplementedError):
-        m(sample(1, 32, 48))
+def test_model_gru_trains():
+    """GRU mode with gradients: the differentiable path (torch prologue, step-level
+    backward kernels) gives the same forward as the fused inference path, and its
+    gradient agrees with a central finite difference of the loss along a random
+    direction in the GRU / decode_aff weights (smooth in them: offsets are fixed)."""
+    torch.manual_seed(0)
+    H, W = 32, 48
+    m = NLSPNModel(make_args(prop_time=4, patch_height=H, patch_width=W)).to(DEV).train()
+    randomize_aff_head(m)
+    for mod in m.modules():  # no batch statistics: forward must be a fixed function of the weights
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.eval()
+    s = sample(2, H, W, seed=7)
+    with torch.no_grad():
+        ref = m(s)
+    out = m(s)
+    d = (out["pred"] - ref["pred"]).norm() / ref["pred"].norm()
+    assert d.item() <= 1e-5
+    gt = torch.rand(2, 1, H, W, device=DEV) * 10
+    loss = ((out["pred"] - gt) ** 2).mean()
+    loss.backward()
+    params = [p for n, p in m.named_parameters() if n.startswith(("GRU.", "decode_aff.", "encode_aff."))]
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in params)
+    assert sum(p.grad.abs().sum().item() for p in params) > 0
+    g = torch.Generator(device=DEV).manual_seed(1)
+    # direction scaled to each tensor's weight magnitude; eps = 1 % of it
+    v = [torch.randn(p.shape, device=DEV, generator=g) * (p.detach().abs().mean() + 1e-3) for p in params]
+    dd = sum((p.grad * u).sum().item() for p, u in zip(params, v))
+    eps = 1e-2
+    with torch.no_grad():
+        def lossv(sign):
+            for p, u in zip(params, v):
+                p.add_(sign * eps * u)
+            r = ((m(s)["pred"] - gt) ** 2).mean().item()
+            for p, u in zip(params, v):
+                p.sub_(sign * eps * u)
+            return r
+        fd = (lossv(1.0) - lossv(-1.0)) / (2 * eps)
+    assert abs(fd - dd) <= 2e-2 * max(abs(dd), 1e-6), (fd, dd)
 
 
 def test_model_trains_end_to_end():
