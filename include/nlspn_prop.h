@@ -97,8 +97,9 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
                     void *p_out, void *pred_out,
                     int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
 
-/* Bytes of device workspace nlspn_propagate needs (currently 0: the prologue is
- * fused into the first iteration; the argument is kept for ABI stability). */
+/* Bytes of device workspace nlspn_propagate uses: the resident kernel's progress
+ * words (one 32-bit word per workgroup + an abort word at index grid).  With a
+ * NULL workspace nlspn_propagate runs iterations 2..T as T-1 launches instead. */
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
 
 /*
@@ -106,7 +107,12 @@ size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
  *   step 1   : the prologue fused into the first iteration — _off_insert (:324)
  *              if off_out, _affinity_normalization (:325), mask_fix / confidence
  *              blend (:328-334), first blend+clamp (:341-348), then iteration 1
- *   steps 2..T: nlspn_prop_step, writing pred_inter[t]; the last also writes pred.
+ *   steps 2..T: ONE resident launch (the invariant planes held on chip for all
+ *              iterations, per-workgroup progress words in `workspace`) when the
+ *              geometry allows it (3x3 learned offsets, W % 4 == 0, 16-B aligned
+ *              planes, every part fits a workgroup: nlspn_resident_config), else
+ *              T-1 nlspn_prop_step launches; pred_inter[t] each, the last also pred.
+ *              Both forms are bit-identical.
  * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
  *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
  *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
@@ -225,6 +231,27 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
                          const void *off, int64_t off_bstride, int off_layout,
                          void *p_out, int B, int H, int W, int kh, int kw, unsigned flags,
                          int reps, void *stream, float *mean_ms, float *min_ms);
+
+/*
+ * Diagnostics: run nlspn_propagate `reps` times with dispatch-recorded HIP events
+ * around every launch, synchronise, and return the mean duration of step 1
+ * (first_ms) and of iterations 2..T (rest_ms: the resident kernel, or the sum of
+ * the T-1 step kernels); *resident = 1 if the resident kernel ran.
+ */
+int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
+                         const void *aff_raw, int64_t aff_bstride, const void *off_raw,
+                         int64_t off_bstride, const float *gamma, void *pred_inter, void *pred,
+                         void *aff_out, void *off_out, void *conf_out, void *workspace,
+                         int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags,
+                         int reps, void *stream, float *first_ms, float *rest_ms, int *resident);
+
+/*
+ * Diagnostics: 1 if nlspn_propagate would run iterations 2..T as the resident
+ * kernel for this shape (given 16-B aligned planes and a workspace), with its
+ * launch shape; 0 otherwise.  Queries the current device's CU count.
+ */
+int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf,
+                          int *grid, int *block, int *lds_bytes);
 
 #ifdef __cplusplus
 }

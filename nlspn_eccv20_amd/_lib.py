@@ -50,6 +50,9 @@ SIGNATURES = {
     "nlspn_prop_step_backward": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _i, _i, _i, _i, _i, _u, _vp]),
     "nlspn_affinity_normalize_backward_workspace_bytes": (_sz, [_i, _i, _i, _i]),
+    "nlspn_time_propagate": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _i, _i, _i, _i, _i, _i, _i, _u, _i, _vp, _vp, _vp, _vp]),
+    "nlspn_resident_config": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "nlspn_affinity_normalize_backward": (_i, [_i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
 }
 

@@ -5,7 +5,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -15,6 +17,7 @@
 #include "nlspn_affnorm.h"
 #include "nlspn_backward.h"
 #include "nlspn_step.h"
+#include "nlspn_resident.h"
 
 using namespace nlspn;
 
@@ -145,6 +148,104 @@ int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = null
     return check_launch("nlspn_prop_step");
 }
 
+// ------------------------------------------------------------ resident dispatch
+// Iterations 2..T in one launch with the invariant planes held on chip
+// (nlspn_resident.h).  Applies to the 3x3 learned-offset geometry when every
+// part's quads fit one workgroup and its window fits LDS; otherwise the T-1
+// per-iteration launches run.  Opt-in (NLSPN_RESIDENT=1) for now.
+constexpr int kResMaxNT = 768;
+constexpr size_t kSyncBytes = 4096;  // progress words + abort word (nlspn_workspace_bytes)
+
+int device_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
+struct ResPlan {
+    const void *fn = nullptr;
+    unsigned grid = 0, block = 0;
+    size_t lds = 0, sync_bytes = 0;
+    ResArgs a{};
+};
+
+template <typename T>
+const void *res_fn(int smax) {
+    return smax == 4 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 4>)
+                     : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 8>);
+}
+
+// Fills P and returns true when the resident kernel applies.
+bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
+                   long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
+                   int kw, int T, unsigned flags, ResPlan &P) {
+    const char *env = getenv("NLSPN_RESIDENT");
+    if (!env || env[0] != '1') return false;  // opt-in while it trails the per-iteration launches at C2
+    if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
+    const size_t es = esize(dtype), vb = 4 * es;
+    if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
+        !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
+        return false;
+    const int cus = device_cus();
+    if (cus < 1 || B > cus) return false;
+    const long long W4 = W / 4, Q = (long long)H * W4;
+    const long long HW = (long long)H * W;
+    if (HW * 9 * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into a 9-plane item
+    // the most parts per image (up to one workgroup per CU) whose quads fit one
+    // workgroup and whose window fits the staging slots and LDS
+    int g = (int)std::min<long long>(cus / B, Q / 64);
+    long long nt = 0, wh_max = 0;
+    int smax = 0;
+    size_t lds = 0;
+    for (; g >= 1; --g) {
+        long long qmax = 0, nsq_max = 0;
+        wh_max = 0;
+        for (int j = 0; j < g; ++j) {
+            const long long qlo = (long long)j * Q / g, qhi = (long long)(j + 1) * Q / g;
+            qmax = std::max(qmax, qhi - qlo);
+            const long long rlo = qlo / W4 - kResRY, rhi = (qhi - 1) / W4 + kResRY;
+            wh_max = std::max(wh_max, rhi - rlo + 1);
+            const long long ra = std::max(rlo, 0LL), rb = std::min(rhi, (long long)H - 1);
+            nsq_max = std::max(nsq_max, (rb - ra + 1) * W4);
+        }
+        nt = (qmax + 63) / 64 * 64;
+        if (nt > kResMaxNT) break;  // fewer parts only makes them larger
+        smax = nsq_max <= 4 * nt ? 4 : (nsq_max <= 8 * nt ? 8 : 0);
+        lds = 16 + sizeof(float) * (size_t)(2 * wh_max * (W + 2 * kResRX)) + 16 * (size_t)(8 + 1) * nt;
+        if (smax && lds <= 160 * 1024) break;
+    }
+    if (g < 1 || nt > kResMaxNT || !smax || lds > 160 * 1024) return false;
+    lds = std::max(lds, (size_t)(80 * 1024 + 16));  // > half a CU's LDS: one workgroup per CU
+    const unsigned G = (unsigned)(B * g);
+    if ((G + 1) * 4 > kSyncBytes) return false;
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(smax) : res_fn<__half>(smax);
+    P.grid = G;
+    P.block = (unsigned)nt;
+    P.lds = lds;
+    P.sync_bytes = ((G + 1) * 4 + 15) / 16 * 16;
+    P.a = ResArgs{conf_eff, (flags & kPreserve) ? dep : nullptr, aff_norm, off_raw, pred_inter, pred,
+                  static_cast<unsigned *>(workspace), off_bs, B, H, W, T, g, (int)wh_max, flags, 0u};
+    if (const char *d = getenv("NLSPN_RES_DBG")) P.a.dbg = (unsigned)atoi(d);
+    return true;
+}
+
+int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
+    NLSPN_HIP_TRY(hipMemsetAsync(P.a.sync, 0, P.sync_bytes, s));
+    void *args[] = {&P.a};
+    if (e0)
+        NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s, e0, e1, 0));
+    else
+        NLSPN_HIP_TRY(hipLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s));
+    return check_launch("nlspn_propagate resident");
+}
+
 // ------------------------------------------------------- affinity-normalisation dispatch
 template <typename T, int K>
 const void *affnorm_fn(bool vec) {
@@ -212,6 +313,72 @@ unsigned elementwise_grid(long long groups) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
+// The whole section (see nlspn_propagate).  ev (optional, 2*T events): a dispatch-
+// recorded pair around each launch — [0,1] step 1, then [2,3] the resident kernel
+// or [2t, 2t+1] per-iteration step t+1.  *resident (optional): 1 if the resident
+// kernel ran iterations 2..T.
+int propagate_impl(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
+                   int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
+                   void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out, void *workspace,
+                   int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags, hipStream_t s,
+                   hipEvent_t *ev, int *resident) {
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
+        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
+    if (!pred_init || !aff_raw || !gamma || !pred_inter || !pred || !aff_out)
+        return fail(NLSPN_EINVAL, "null required pointer");
+    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    if (conf && !conf_out) return fail(NLSPN_EINVAL, "conf given without conf_out");
+    if (off_out && !off_raw) return fail(NLSPN_EINVAL, "off_out given without off_raw");
+    const int K = kh * kw - 1;
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
+    if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
+    const size_t es = esize(dtype);
+
+    // iteration 1 with the prologue fused in (raw head outputs in, output-dict
+    // tensors out), then T-1 steps on the normalised affinity and conf'
+    StepReq r1{};
+    r1.dtype = dtype;
+    r1.kh = kh;
+    r1.kw = kw;
+    r1.first = true;
+    r1.a = StepArgs{pred_init, conf, dep, aff_raw, off_raw, pred_inter, T == 1 ? pred : nullptr,
+                    aff_bstride, off_bstride, B, H, W, 0, 0, 1, flags, gamma, aff_out, off_out,
+                    conf ? conf_out : nullptr, kind};
+    StepLaunch L1;
+    int rc = prepare_step(r1, L1);
+    if (rc) return rc;
+    StepReq r{};
+    r.dtype = dtype;
+    r.kh = kh;
+    r.kw = kw;
+    r.a = StepArgs{pred_inter, conf ? conf_out : nullptr, dep, aff_out, off_raw, pred_inter, pred,
+                   (long long)(K + 1) * HW, off_bstride, B, H, W, 0, 0, 1, flags, nullptr, nullptr, nullptr, nullptr, 0};
+    StepLaunch L;
+    if (T > 1 && (rc = prepare_step(r, L))) return rc;
+
+    if (resident) *resident = 0;
+    if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
+    ResPlan P;
+    if (plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter, pred,
+                      workspace, B, H, W, kh, kw, T, flags, P)) {
+        if (resident) *resident = 1;
+        return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    }
+    for (int t = 1; t < T; ++t) {  // list_pred[t] lands in pred_inter[t]
+        StepArgs a = r.a;
+        a.p_in = static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
+        a.p_out = static_cast<char *>(pred_inter) + (size_t)t * N * es;
+        a.pred_out = t == T - 1 ? pred : nullptr;
+        if ((rc = launch(L, a, s, ev ? ev[2 * t] : nullptr, ev ? ev[2 * t + 1] : nullptr))) return rc;
+    }
+    return NLSPN_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -257,63 +424,16 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
 
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W) {
     (void)dtype; (void)B; (void)H; (void)W;
-    return 0;  // the prologue is fused into the first iteration; no scratch plane is needed
+    return kSyncBytes;  // the resident kernel's progress words (the prologue needs no scratch)
 }
 
 int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
                     int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
                     void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out, void *workspace,
                     int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags, void *stream) {
-    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
-    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
-    if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
-    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
-    if (kh < 1 || kw < 1 || (kh % 2) == 0 || (kw % 2) == 0 || kh * kw < 2)
-        return fail(NLSPN_EINVAL, "only odd kernel is supported but k = %dx%d", kh, kw);
-    if (!pred_init || !aff_raw || !gamma || !pred_inter || !pred || !aff_out)
-        return fail(NLSPN_EINVAL, "null required pointer");
-    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
-    if (conf && !conf_out) return fail(NLSPN_EINVAL, "conf given without conf_out");
-    if (off_out && !off_raw) return fail(NLSPN_EINVAL, "off_out given without off_raw");
-    const int K = kh * kw - 1;
-    const long long HW = (long long)H * W, N = (long long)B * HW;
-    if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
-    if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
-    hipStream_t s = as_stream(stream);
-    const size_t es = esize(dtype);
-
-    // iteration 1 with the prologue fused in (raw head outputs in, output-dict
-    // tensors out), then T-1 steps on the normalised affinity and conf'
-    StepReq r1{};
-    r1.dtype = dtype;
-    r1.kh = kh;
-    r1.kw = kw;
-    r1.first = true;
-    r1.a = StepArgs{pred_init, conf, dep, aff_raw, off_raw, pred_inter, T == 1 ? pred : nullptr,
-                    aff_bstride, off_bstride, B, H, W, 0, 0, 1, flags, gamma, aff_out, off_out,
-                    conf ? conf_out : nullptr, kind};
-    StepLaunch L1;
-    int rc = prepare_step(r1, L1);
-    if (rc) return rc;
-    StepReq r{};
-    r.dtype = dtype;
-    r.kh = kh;
-    r.kw = kw;
-    r.a = StepArgs{pred_inter, conf ? conf_out : nullptr, dep, aff_out, off_raw, pred_inter, pred,
-                   (long long)(K + 1) * HW, off_bstride, B, H, W, 0, 0, 1, flags, nullptr, nullptr, nullptr, nullptr, 0};
-    StepLaunch L;
-    if (T > 1 && (rc = prepare_step(r, L))) return rc;
-    (void)workspace;
-
-    if ((rc = launch(L1, r1.a, s))) return rc;
-    for (int t = 1; t < T; ++t) {  // list_pred[t] lands in pred_inter[t]
-        StepArgs a = r.a;
-        a.p_in = static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
-        a.p_out = static_cast<char *>(pred_inter) + (size_t)t * N * es;
-        a.pred_out = t == T - 1 ? pred : nullptr;
-        if ((rc = launch(L, a, s))) return rc;
-    }
-    return NLSPN_OK;
+    return propagate_impl(dtype, pred_init, dep, conf, aff_raw, aff_bstride, off_raw, off_bstride, gamma, pred_inter,
+                          pred, aff_out, off_out, conf_out, workspace, B, H, W, kh, kw, T, kind, flags,
+                          as_stream(stream), nullptr, nullptr);
 }
 
 struct nlspn_plan {
@@ -640,6 +760,61 @@ int nlspn_affinity_normalize_backward(int dtype, const void *aff_raw, int64_t af
         return check_launch("nlspn_affinity_normalize_backward gamma");
     }
     return NLSPN_OK;
+}
+
+int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
+                         int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
+                         void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out, void *workspace,
+                         int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags, int reps, void *stream,
+                         float *first_ms, float *rest_ms, int *resident) {
+    if (reps < 1 || T < 1 || !first_ms || !rest_ms) return fail(NLSPN_EINVAL, "reps/T must be >= 1, outputs non-null");
+    hipStream_t s = as_stream(stream);
+    std::vector<hipEvent_t> ev(2 * (size_t)T * reps, nullptr);
+    int rc = NLSPN_OK;
+    for (auto &e : ev)
+        if (hipEventCreate(&e) != hipSuccess) rc = fail(NLSPN_EHIP, "hipEventCreate failed");
+    int res = 0;
+    for (int i = 0; i < reps && rc == 0; ++i)
+        rc = propagate_impl(dtype, pred_init, dep, conf, aff_raw, aff_bstride, off_raw, off_bstride, gamma, pred_inter,
+                            pred, aff_out, off_out, conf_out, workspace, B, H, W, kh, kw, T, kind, flags, s,
+                            ev.data() + 2 * (size_t)T * i, &res);
+    double f = 0.0, r = 0.0;
+    if (rc == 0) {
+        hipError_t se = hipStreamSynchronize(s);
+        if (se != hipSuccess) rc = fail(NLSPN_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(se));
+    }
+    for (int i = 0; i < reps && rc == 0; ++i) {
+        hipEvent_t *e = ev.data() + 2 * (size_t)T * i;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e[0], e[1]) != hipSuccess) { rc = fail(NLSPN_EHIP, "hipEventElapsedTime"); break; }
+        f += ms;
+        const int nrest = T < 2 ? 0 : (res ? 1 : T - 1);
+        for (int k = 1; k <= nrest && rc == 0; ++k) {
+            if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) != hipSuccess) rc = fail(NLSPN_EHIP, "hipEventElapsedTime");
+            r += ms;
+        }
+    }
+    for (auto &e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (rc) return rc;
+    *first_ms = (float)(f / reps);
+    *rest_ms = (float)(r / reps);
+    if (resident) *resident = res;
+    return NLSPN_OK;
+}
+
+int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf, int *grid,
+                          int *block, int *lds_bytes) {
+    ResPlan P;
+    alignas(16) static char dummy[16];
+    void *d = dummy;
+    if (!plan_resident(dtype, has_conf ? d : nullptr, d, d, d, 2LL * (kh * kw - 1) * H * W, d, d, d, B, H, W, kh,
+                       kw, T, NLSPN_PRESERVE_INPUT, P))
+        return 0;
+    if (grid) *grid = (int)P.grid;
+    if (block) *block = (int)P.block;
+    if (lds_bytes) *lds_bytes = (int)P.lds;
+    return 1;
 }
 
 }  // extern "C"

@@ -1,0 +1,410 @@
+// Resident propagation: iterations 2..T of the NLSPN loop in ONE launch, with
+// every iteration-invariant plane held on chip.
+//
+// Why: a per-iteration launch (nlspn_step.h) must re-read the invariant planes
+// — K normalised affinities, 2K offsets, conf', dep: 27 fp32 planes = 108 of its
+// 112 B/px at K=8 — every iteration, so it is HBM-bound at ~6 TB/s however it is
+// tiled.  Those planes do not change between iterations (nlspnmodel.py:340-363
+// re-uses offset / aff / confidence / dep), and at NYU size (C2: 60 MB) they fit
+// in the register files (128 MB chip-wide).  So this kernel keeps them there:
+//
+//   * one workgroup per CU owns a contiguous run of pixel quads of ONE image
+//     (image b = blockIdx % B, part j = blockIdx / B, so an image's parts share
+//     an XCD group); each thread owns one quad (4 pixels of a row) and holds its
+//     26 invariant words per pixel (8 affinities, the reference-tap weight
+//     1 - sum, 16 offsets, dep) in VGPRs for the whole launch;
+//   * the part's conf' window (its rows +- RY, the full width +- RX, zero
+//     outside the image) lives in LDS for the whole launch;
+//   * per iteration only the previous depth plane moves: the window rows of
+//     p_{t-1} are loaded (write-through hand-off, below), multiplied by conf'
+//     into the LDS f-window, the taps are sampled exactly as prop_step_kernel
+//     does (same IEEE sequence: bit-identical), and p_t is stored.
+//
+// Between iterations a part waits only for the parts its window (and any
+// out-of-window tap) reads — a contiguous range of parts of its own image,
+// computed once from the invariant offsets — through per-workgroup progress
+// words.  Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, the
+// write-through row of MI355X_MICROARCH.md § inter-workgroup visibility):
+//   producer: every p_t store is `sc1` (write-through), every wave drains
+//             (s_waitcnt vmcnt(0)), workgroup barrier, ONE lane stores its
+//             progress word = t (relaxed, agent scope = sc1 store);
+//   consumer: ONE wave polls the words it depends on (relaxed sc1 loads),
+//             workgroup barrier, then EVERY load of a pred_inter plane is an
+//             `sc1` load (no acquire fence needed, L1 bypassed).
+// Loads of bytes not written in this launch (conf', invariants) are plain.
+// Every plane t is written once, so there is no write-after-read hazard and a
+// fast part may run ahead of parts that do not feed it.
+//
+// Residency: G = B * g workgroups (g parts per image), at most one per CU (the
+// dynamic LDS request exceeds half a CU's LDS) and G <= CU count, so the whole
+// grid is resident.  Every spin is bounded: on timeout a part raises the abort
+// word (sync[G]) and every part exits; outputs are then invalid and the abort
+// word stays set for the host to inspect.
+#pragma once
+
+#include "nlspn_common.h"
+#include "nlspn_step.h"
+
+namespace nlspn {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+struct ResArgs {
+    const void *conf;   // conf' (B planes) or null (conf_prop off)
+    const void *dep;    // B planes or null (preserve off)
+    const void *aff;    // normalised affinity, (K+1) planes per item, contiguous (aff_out)
+    const void *off;    // raw offsets, 2K planes per item, batch stride off_bs
+    void *pred_inter;   // T x B planes: iteration t reads plane t-1, writes plane t
+    void *pred;         // B planes: max(p_T, 0) (nlspnmodel.py:375-377)
+    unsigned *sync;     // [G] progress words, [G] abort word; zeroed before every launch
+    long long off_bs;   // elements
+    int B, H, W, T;
+    int g;              // parts (workgroups) per image
+    int wh_max;         // LDS window rows allocated per buffer
+    unsigned flags;
+    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps
+};
+
+constexpr int kResRY = 8, kResRX = 8;            // window halo (rows, columns)
+constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
+constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
+
+// Part j of an image with Q quads owns quads [j*Q/g, (j+1)*Q/g); owner(q) is the
+// largest j with floor(j*Q/g) <= q.
+__device__ __forceinline__ int res_owner(long long q, long long Q, int g) {
+    return (int)(((q + 1) * g - 1) / Q);
+}
+
+template <typename T> struct ResVec;  // 4 contiguous elements <-> float[4], buffer access with cache bits
+template <> struct ResVec<float> {
+    template <unsigned AUX>
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[4]) {
+        const f32x4 q = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, AUX));
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
+        const f32x4 q = {v[0], v[1], v[2], v[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q), r, vo, so, AUX);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ float load1(rsrc_t r, unsigned vo, unsigned so) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, AUX));
+    }
+};
+template <> struct ResVec<__half> {
+    template <unsigned AUX>
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[4]) {
+        const f16x4 q = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, AUX));
+        v[0] = (float)q[0]; v[1] = (float)q[1]; v[2] = (float)q[2]; v[3] = (float)q[3];
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
+        const f16x4 q = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, AUX);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ float load1(rsrc_t r, unsigned vo, unsigned so) {
+        return (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, AUX));
+    }
+};
+
+// 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
+// MAXNT = launch bound (threads), SMAX = staging quads per thread per iteration.
+template <typename T, int MAXNT, int SMAX>
+__global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
+    constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RX = kResRX;
+    constexpr unsigned ES = sizeof(T);
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    int *ctl = reinterpret_cast<int *>(smem);  // [0] abort, [1] min dep row, [2] max dep row
+    const int H = a.H, W = a.W, WW = W + 2 * RX, W4 = W / 4;
+    float *fwin = smem + 4;
+    float *cwin = fwin + (size_t)a.wh_max * WW;
+    float4 *akl = reinterpret_cast<float4 *>(cwin + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
+    const int NT = blockDim.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+
+    const int b = blockIdx.x % a.B, j = blockIdx.x / a.B;
+    const long long Q = (long long)H * W4;
+    const long long qlo = (long long)j * Q / a.g, qhi = (long long)(j + 1) * Q / a.g;
+    const int rlo = (int)(qlo / W4) - RY, rhi = (int)((qhi - 1) / W4) + RY;  // window rows (inclusive)
+    const int WH = rhi - rlo + 1;
+    const int ra = rlo < 0 ? 0 : rlo, rb = rhi > H - 1 ? H - 1 : rhi;      // in-image window rows
+    const int nsq = (rb - ra + 1) * W4;                                    // staging quads per iteration
+
+    const bool has_conf = a.conf != nullptr;
+    const bool preserve = (a.flags & kPreserve) != 0;
+    const bool clip = (a.flags & kAlwaysClip) != 0;
+    const long long HW = (long long)H * W, N = (long long)a.B * HW;
+    const unsigned plane_bytes = (unsigned)HW * ES;
+    gu32 *sync = (gu32 *)(a.sync);
+    const int G = gridDim.x;
+
+    // ---- own quad and its invariants (registers for the whole launch).  Taps are
+    // held as their sample coordinates (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw),
+    // the reference's own expression (.cuh:178-179), so an iteration starts from them.
+    const long long q = qlo + tid;
+    const bool active = q < qhi;
+    const int y = active ? (int)(q / W4) : 0, x0 = active ? (int)(q % W4) * 4 : 0;
+    const unsigned vpix = (unsigned)(y * W + x0) * ES;
+    float hy[K][4], hx[K][4], dv[4];
+    {
+        float ak[K][4], aref[4];
+        const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
+        const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, ak[k]);
+            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * k) * plane_bytes, hy[k]);
+            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * k + 1) * plane_bytes, hx[k]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[e] = 0.f;
+        if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
+            float s = 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) s += ak[k][e];
+            aref[e] = 1.0f - s;
+        }
+        // the affinities are consumed last in a tap, so they wait in LDS (conflict-
+        // free 16-B rows per thread) and leave the registers to the tap coordinates
+#pragma unroll
+        for (int k = 0; k < K; ++k) akl[k * NT + tid] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
+        akl[K * NT + tid] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+    }
+
+    // ---- LDS init: f-window zero (cells outside the image stay 0 = zero padding),
+    // conf' window for the in-image cells (invariant), dependency rows
+    if (tid == 0) { ctl[0] = 0; ctl[1] = ra; ctl[2] = rb; }
+    for (int i = tid; i < WH * WW; i += NT) fwin[i] = 0.f;
+    if (has_conf) {
+        const rsrc_t rc = make_rsrc(static_cast<const T *>(a.conf) + b * HW);
+        for (int i = tid; i < nsq; i += NT) {
+            const int r = ra + i / W4, c = (i % W4) * 4;
+            float v[4];
+            ResVec<T>::template load<0>(rc, (unsigned)(r * W + c) * ES, 0u, v);
+            *reinterpret_cast<float4 *>(&cwin[(r - rlo) * WW + RX + c]) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+    __syncthreads();
+    // Classify every tap once (offsets are invariant):
+    //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
+    //    coordinates are redirected to (rlo, -RX), an integer point of the window's
+    //    zero padding columns, so the branch-free path reads four zeros with weights
+    //    (1,0,0,0): v = +0 exactly, as the reference's val = 0;
+    //  * in the LDS window: the branch-free path;
+    //  * valid but outside the window: read from global memory by the general path
+    //    (has_fb), and the dependency rows are widened to cover it.
+    const float Hf = (float)H, Wf = (float)W;
+    bool has_fb = false;
+    {
+        int mn = H, mx = -1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float h_im = (float)(y - PH + i) + hy[k][e];
+                const float w_im = (float)(x0 + e - PW + jj) + hx[k][e];
+                hy[k][e] = h_im;
+                hx[k][e] = w_im;
+                if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                    const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                    const int ry = h_low - rlo, rx = w_low + RX;
+                    if (!((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1))) {
+                        has_fb = true;
+                        mn = min(mn, max(h_low, 0));
+                        mx = max(mx, min(h_low + 1, H - 1));
+                    }
+                } else {
+                    hy[k][e] = (float)rlo;
+                    hx[k][e] = -(float)RX;
+                }
+            }
+        }
+        has_fb = has_fb && active;
+        if (has_fb) { atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); }
+    }
+    __syncthreads();
+    const int jlo = res_owner((long long)ctl[1] * W4, Q, a.g);
+    const int jhi = res_owner((long long)(ctl[2] + 1) * W4 - 1, Q, a.g);
+    const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
+
+    const T *p_all = static_cast<const T *>(a.pred_inter);
+    T *p_out_all = static_cast<T *>(a.pred_inter);
+    const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
+
+    for (int t = 1; t < a.T; ++t) {
+        // The tap geometry depends only on the (invariant) coordinates, so the
+        // compiler would hoist all 32 taps' weights and addresses out of this loop
+        // and spill them; opaque register moves keep them per iteration (no code).
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(hy[k][e]), "+v"(hx[k][e]));
+        int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
+        asm volatile("" : "+v"(tb));
+
+        // ---- wait until every part this one reads has finished iteration t-1
+        if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
+            unsigned spins = 0;
+            bool fail = false;
+            for (int base = jlo; base <= jhi && !fail; base += 64) {
+                const int jj = base + lane;
+                for (;;) {
+                    bool ok = true;
+                    if (jj <= jhi)
+                        ok = __hip_atomic_load(&sync[jj * a.B + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                             (unsigned)(t - 1);
+                    if (__all(ok)) break;
+                    if (++spins > kResSpinLimit ||
+                        __hip_atomic_load(&sync[G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                        fail = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if (fail && lane == 0) {
+                ctl[0] = 1;
+                __hip_atomic_store(&sync[G], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
+        if (ctl[0]) return;
+
+        // ---- stage f = p_{t-1} * conf' for the in-image window cells (sc1 loads)
+        const T *p_in = p_all + (size_t)(t - 1) * N + b * HW;
+        const rsrc_t rp = make_rsrc(p_in);
+        float sv[SMAX][4];
+        const int nsq_it = (a.dbg & 2u) ? 0 : nsq;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+            const int i = tb + s * NT;
+            if (i < nsq_it) {
+                const int r = ra + i / W4, c = (i % W4) * 4;
+                ResVec<T>::template load<kSc1>(rp, (unsigned)(r * W + c) * ES, 0u, sv[s]);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+            const int i = tb + s * NT;
+            if (i < nsq_it) {
+                const int r = ra + i / W4, c = (i % W4) * 4;
+                const int li = (r - rlo) * WW + RX + c;
+                float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
+                if (has_conf) {
+                    const float4 cc = *reinterpret_cast<const float4 *>(&cwin[li]);
+                    f.x = f.x * cc.x; f.y = f.y * cc.y; f.z = f.z * cc.z; f.w = f.w * cc.w;
+                }
+                *reinterpret_cast<float4 *>(&fwin[li]) = f;
+            }
+        }
+        lds_barrier();
+
+        // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
+        if (active && !(a.dbg & 4u)) {
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            // branch-free path: every tap from the LDS window (invalid taps read zeros)
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (k == REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
+                    const float4 ar = akl[K * NT + tid];
+                    const float *c = &fwin[(y - rlo) * WW + x0 + RX];
+                    acc[0] += c[0] * ar.x; acc[1] += c[1] * ar.y; acc[2] += c[2] * ar.z; acc[3] += c[3] * ar.w;
+                }
+                const float4 a4 = akl[k * NT + tid];
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float h_im = hy[k][e], w_im = hx[k][e];
+                    const float fh = floorf(h_im), fw = floorf(w_im);
+                    const float lh = h_im - fh, lw = w_im - fw;  // = h - (float)h_low (.cuh:35-36)
+                    const float hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    const float *sp = &fwin[((int)fh - rlo) * WW + (int)fw + RX];
+                    const float v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
+                    acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
+                }
+            }
+            // general path (rare; only waves holding a tap outside the window): the
+            // reference's per-corner checks, from global memory where needed.  It
+            // re-reads its offsets from global memory and runs a rolled tap loop, so it
+            // shares no registers with the branch-free path (no spills around it).
+            if (wave_fb && has_fb) {
+                const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float s = 0.f;
+#pragma unroll 1
+                    for (int k = 0; k < K; ++k) {
+                        if (k == REF) {
+                            const float4 ar = akl[K * NT + tid];
+                            const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
+                            s += fwin[(y - rlo) * WW + x0 + e + RX] * arv[e];
+                        }
+                        const float4 a4 = akl[k * NT + tid];
+                        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                        const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
+                        const float h_im = (float)(y - PH + i) +
+                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * k) * plane_bytes);
+                        const float w_im = (float)(x0 + e - PW + jj) +
+                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * k + 1) * plane_bytes);
+                        float v = 0.f;
+                        if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                            const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                            const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                            const float hh = 1.f - lh, hw = 1.f - lw;
+                            const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                            const int ry = h_low - rlo, rx = w_low + RX;
+                            if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
+                                const float *sp = &fwin[ry * WW + rx];
+                                v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
+                            } else {
+                                const int h_high = h_low + 1, w_high = w_low + 1;
+                                float c4[4];
+                                const int cy[4] = {h_low, h_low, h_high, h_high};
+                                const int cx[4] = {w_low, w_high, w_low, w_high};
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    c4[u] = 0.f;
+                                    if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
+                                        const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
+                                        const float pv = ResVec<T>::template load1<kSc1>(rp, qo, 0u);
+                                        c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                                    }
+                                }
+                                v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
+                            }
+                        }
+                        s += v * av[e];
+                    }
+                    acc[e] = s;
+                }
+            }
+            float o[4], fin[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float vv = acc[e];
+                if (preserve) {  // :355-357
+                    const float m = dv[e] > 0.f ? 1.f : 0.f;
+                    vv = (1.0f - m) * vv + m * dv[e];
+                }
+                if (clip) vv = clamp0(vv);  // :359-361
+                o[e] = vv;
+                fin[e] = clip ? vv : clamp0(vv);  // :375-377
+            }
+            T *p_out = p_out_all + (size_t)t * N + b * HW;
+            ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);
+            if (t == a.T - 1) ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
+        }
+        // ---- publish: every wave drains its write-through stores, then ONE lane
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(&sync[blockIdx.x], (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+}  // namespace nlspn

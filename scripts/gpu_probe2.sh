@@ -1,0 +1,4 @@
+set -o pipefail
+O=gpurun_out; mkdir -p $O
+timeout -k 10 300 python -m pytest tests/test_gpu_resident.py -x -q -p no:cacheprovider > $O/pytest_resident.log 2>&1 &&
+bash scripts/gpu_probe_pmc.sh

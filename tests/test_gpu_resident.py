@@ -1,0 +1,150 @@
+"""GPU: the resident propagation kernel (iterations 2..T in one launch, invariant
+planes on chip, per-workgroup progress words) against the per-iteration launches
+and the oracle.
+
+Bar: BIT-EXACT against the T-1 per-iteration launches (both issue the same IEEE
+sequence per pixel; only the schedule and the hand-off differ), every one of the
+T pred_inter planes, and no abort raised.  Exercised where hand-offs are most
+fragile: long-range offsets (dependency ranges over many parts, taps beyond the
+LDS window), tiny parts, repeated graph replays (a stale read shows up as a
+replay that differs), fp16 storage, and every flag combination.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nlspn_eccv20_amd import PropagationPlan, _lib, propagate
+from nlspn_eccv20_amd.synthetic import rmse, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def cu(x, dtype=torch.float32):
+    return None if x is None else torch.from_numpy(np.ascontiguousarray(x)).to(DEV, dtype)
+
+
+def resident_config(B, H, W, dtype=0, conf=True, T=18):
+    g, b, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    ok = _lib.get().nlspn_resident_config(dtype, B, H, W, 3, 3, T, int(conf), ctypes.byref(g), ctypes.byref(b),
+                                          ctypes.byref(l))
+    return bool(ok), g.value, b.value, l.value
+
+
+class _env:
+    def __init__(self, value):
+        self.value = value
+
+    def __enter__(self):
+        self.old = os.environ.get("NLSPN_RESIDENT")
+        os.environ["NLSPN_RESIDENT"] = self.value
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("NLSPN_RESIDENT", None)
+        else:
+            os.environ["NLSPN_RESIDENT"] = self.old
+
+
+def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=0.05):
+    s = synth(B, H, W, 8, seed=seed, off_sigma=sigma, density=density)
+    oa = cu(s["off_aff"], dtype)
+    return (cu(s["pred_init"], dtype), cu(s["dep"], dtype), cu(s["conf"], dtype) if conf else None,
+            oa[:, 16:], oa[:, :16], torch.tensor([4.0], device=DEV)), s
+
+
+def _both(inp, T=18, **kw):
+    with _env("1"):
+        a = propagate(*inp, prop_time=T, **kw)
+    with _env("0"):
+        b = propagate(*inp, prop_time=T, **kw)
+    torch.cuda.synchronize()
+    return a, b
+
+
+def test_resident_engaged_at_c2():
+    with _env("1"):
+        ok, grid, block, lds = resident_config(8, 228, 304)
+        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
+        assert not resident_config(4, 240, 1216)[0]      # C3: parts exceed one workgroup
+        assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
+
+
+@pytest.mark.parametrize("B,H,W,sigma,dtype,conf,kw", [
+    (8, 228, 304, 2.0, torch.float32, True, {}),                        # C2
+    (8, 228, 304, 2.0, torch.float32, True, {"always_clip": True}),
+    (8, 228, 304, 2.0, torch.float32, False, {"preserve_input": False}),
+    (8, 228, 304, 2.0, torch.float16, True, {}),                        # fp16 storage
+    (4, 96, 128, 12.0, torch.float32, True, {}),                        # taps beyond the halo
+    (2, 64, 96, 60.0, torch.float32, True, {"affinity": "TC"}),         # mostly out of image, long ranges
+    (1, 24, 32, 2.0, torch.float32, True, {}),                          # 3 tiny parts
+    (32, 40, 64, 2.0, torch.float32, True, {"affinity": "ASS"}),        # many images, 8 parts each
+    (3, 50, 100, 4.0, torch.float32, True, {"affinity": "AS"}),         # B not dividing the CU count
+])
+def test_resident_bitexact_vs_steps(B, H, W, sigma, dtype, conf, kw):
+    with _env("1"):
+        assert resident_config(B, H, W, 0 if dtype == torch.float32 else 1, conf)[0]
+    inp, _ = _inputs(B, H, W, sigma=sigma, dtype=dtype, conf=conf)
+    a, b = _both(inp, **kw)
+    assert torch.equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
+    assert torch.equal(a["pred"], b["pred"])
+
+
+def test_resident_nonfinite_offsets():
+    inp, _ = _inputs(2, 64, 128)
+    off = inp[4].clone()
+    off[0, 3, 5, 7] = float("nan")
+    off[1, 0, 10, 11] = float("inf")
+    off[1, 9, 40, 12] = -1e30
+    inp = inp[:4] + (off, inp[5])
+    a, b = _both(inp)
+    assert torch.equal(a["pred_inter_tensor"].nan_to_num(7.0), b["pred_inter_tensor"].nan_to_num(7.0))
+
+
+def test_resident_replays_stable_and_no_abort():
+    """A hand-off that could read a stale plane shows up as a replay that differs."""
+    inp, _ = _inputs(8, 228, 304, sigma=3.0, seed=11)
+    with _env("0"):
+        ref = propagate(*inp, prop_time=18)["pred_inter_tensor"].clone()
+    with _env("1"):
+        plan = PropagationPlan(*inp, prop_time=18)
+        for i in range(30):
+            o = plan.replay()
+            if i % 5 == 0:  # uneven load between replays: a busy stream beside the plan
+                x = torch.randn(4096, 4096, device=DEV)
+                _ = x @ x
+            torch.cuda.synchronize()
+            assert torch.equal(o["pred_inter_tensor"], ref), f"replay {i} differs"
+            grid = resident_config(8, 228, 304)[1]
+            assert grid > 0
+            assert int(plan.outputs["workspace"][grid].item()) == 0, "resident kernel aborted"
+        plan.close()
+
+
+def test_resident_vs_oracle_c2(oracle):
+    inp, s = _inputs(8, 228, 304, seed=7240)
+    with _env("1"):
+        o = propagate(*inp, prop_time=18)
+    e = oracle.propagate(s["pred_init"], s["dep"], s["conf"], s["off_aff"][:, 16:], s["off_aff"][:, :16], 4.0)
+    assert rmse(o["pred"].cpu().numpy(), e["pred"]) <= 1e-4
+
+
+def test_time_propagate_reports_resident():
+    inp, _ = _inputs(8, 228, 304)
+    os.environ["NLSPN_RESIDENT"] = "1"
+    plan = PropagationPlan(*inp, prop_time=18)
+    o = plan.outputs
+    first, rest, res = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+    pi, dep, conf, aff, off, g = inp
+    _lib.check(_lib.get().nlspn_time_propagate(
+        0, pi.data_ptr(), dep.data_ptr(), conf.data_ptr(), aff.data_ptr(), aff.stride(0), off.data_ptr(),
+        off.stride(0), g.data_ptr(), o["pred_inter"].data_ptr(), o["pred"].data_ptr(), o["aff"].data_ptr(),
+        o["offset"].data_ptr(), o["confidence"].data_ptr(), o["workspace"].data_ptr(), 8, 228, 304, 3, 3, 18, 3,
+        _lib.PRESERVE_INPUT, 3, torch.cuda.current_stream().cuda_stream, ctypes.byref(first), ctypes.byref(rest),
+        ctypes.byref(res)))
+    os.environ.pop("NLSPN_RESIDENT", None)
+    assert res.value == 1 and first.value > 0 and rest.value > 0
+    plan.close()
