@@ -220,6 +220,24 @@ int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const v
                        int group, int deformable_group, void *stream);
 
 /*
+ * Modulated DCNv2 backward, seam 2 (DCN.modulated_deform_conv_backward,
+ * src/model/deformconv/src/vision.cpp:10, modulated_deform_conv.h:46-86,
+ * cuda/modulated_deform_conv_cuda.cu:124-280), float32.  Same layouts as
+ * nlspn_mdcn_forward; grad_output (B, Cout, Ho, Wo).  Writes grad_input (zeroed
+ * here, then scattered with float atomics as the reference's col2im, so its last
+ * bits depend on arrival order), grad_offset, grad_mask, grad_weight and — if
+ * non-NULL — grad_bias.  Reproduces the reference's col2im call passing pad_h for
+ * pad_w (.cuh:371): identical results for square padding, the reference's own
+ * (shifted) grad_input otherwise.  No im2col_step batch-divisibility restriction.
+ */
+int nlspn_mdcn_backward(int dtype, const void *input, const void *weight, const void *offset,
+                        const void *mask, const void *grad_output, void *grad_input,
+                        void *grad_offset, void *grad_mask, void *grad_weight, void *grad_bias,
+                        int B, int C, int H, int W, int Cout, int kh, int kw,
+                        int sh, int sw, int ph, int pw, int dh, int dw,
+                        int group, int deformable_group, void *stream);
+
+/*
  * Diagnostics (not part of the reference surface): enqueue `reps` back-to-back
  * nlspn_prop_step launches on `stream`, each bracketed by its own HIP event
  * pair recorded by the dispatch itself (hipExtLaunchKernelGGL start/stop

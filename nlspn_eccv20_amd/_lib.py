@@ -41,6 +41,8 @@ SIGNATURES = {
     "nlspn_plan_destroy": (_i, [_vp]),
     "nlspn_mdcn_forward": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                                 _i, _i, _i, _i, _vp]),
+    "nlspn_mdcn_backward": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
+                                 _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nlspn_time_prop_step": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i, _vp, _i, _i, _i, _i, _i, _u, _i,
                                   _vp, _fp, _fp]),
     "nlspn_backward_workspace_bytes": (_sz, [_i, _i, _i, _i, _i]),

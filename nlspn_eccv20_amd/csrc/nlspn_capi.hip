@@ -176,9 +176,8 @@ struct ResPlan {
 };
 
 template <typename T>
-const void *res_fn(int smax) {
-    return smax == 4 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 4>)
-                     : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 8>);
+const void *res_fn() {
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 4>);
 }
 
 // Fills P and returns true when the resident kernel applies.
@@ -198,33 +197,31 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const long long HW = (long long)H * W;
     if (HW * 9 * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into a 9-plane item
     // the most parts per image (up to one workgroup per CU) whose quads fit one
-    // workgroup and whose window fits the staging slots and LDS
+    // workgroup; LDS: the f window (as many rows as fit, at least the part's rows
+    // + 2 RY) and the per-thread affinity rows
+    constexpr size_t kLdsBytes = 160 * 1024;
+    const long long WWb = 4LL * (W + 2 * kResRX);
     int g = (int)std::min<long long>(cus / B, Q / 64);
     long long nt = 0, wh_max = 0;
-    int smax = 0;
-    size_t lds = 0;
     for (; g >= 1; --g) {
-        long long qmax = 0, nsq_max = 0;
-        wh_max = 0;
+        long long qmax = 0, rows_max = 0;
         for (int j = 0; j < g; ++j) {
             const long long qlo = (long long)j * Q / g, qhi = (long long)(j + 1) * Q / g;
             qmax = std::max(qmax, qhi - qlo);
-            const long long rlo = qlo / W4 - kResRY, rhi = (qhi - 1) / W4 + kResRY;
-            wh_max = std::max(wh_max, rhi - rlo + 1);
-            const long long ra = std::max(rlo, 0LL), rb = std::min(rhi, (long long)H - 1);
-            nsq_max = std::max(nsq_max, (rb - ra + 1) * W4);
+            rows_max = std::max(rows_max, (qhi - 1) / W4 - qlo / W4 + 1);
         }
         nt = (qmax + 63) / 64 * 64;
         if (nt > kResMaxNT) break;  // fewer parts only makes them larger
-        smax = nsq_max <= 4 * nt ? 4 : (nsq_max <= 8 * nt ? 8 : 0);
-        lds = 16 + sizeof(float) * (size_t)(2 * wh_max * (W + 2 * kResRX)) + 16 * (size_t)(8 + 1) * nt;
-        if (smax && lds <= 160 * 1024) break;
+        const long long avail = (long long)kLdsBytes - 16 - 16LL * 9 * nt;
+        wh_max = avail > 0 ? avail / WWb : 0;
+        if (wh_max >= rows_max + 2 * kResRY) break;
     }
-    if (g < 1 || nt > kResMaxNT || !smax || lds > 160 * 1024) return false;
-    lds = std::max(lds, (size_t)(80 * 1024 + 16));  // > half a CU's LDS: one workgroup per CU
+    if (g < 1 || nt > kResMaxNT || wh_max < 1) return false;
+    const size_t lds = 16 + (size_t)(wh_max * WWb) + 16 * 9 * (size_t)nt;
+    if (lds > kLdsBytes || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
     const unsigned G = (unsigned)(B * g);
     if ((G + 1) * 4 > kSyncBytes) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(smax) : res_fn<__half>(smax);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>() : res_fn<__half>();
     P.grid = G;
     P.block = (unsigned)nt;
     P.lds = lds;
@@ -515,6 +512,45 @@ int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const v
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(elementwise_grid((long long)B * Cout * Ho * Wo)), dim3(256), args, 0,
                                   as_stream(stream)));
     return check_launch("nlspn_mdcn_forward");
+}
+
+int nlspn_mdcn_backward(int dtype, const void *input, const void *weight, const void *offset, const void *mask,
+                        const void *grad_output, void *grad_input, void *grad_offset, void *grad_mask,
+                        void *grad_weight, void *grad_bias, int B, int C, int H, int W, int Cout, int kh, int kw,
+                        int sh, int sw, int ph, int pw, int dh, int dw, int group, int deformable_group,
+                        void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the DCN backward is implemented for float32");
+    if (!input || !weight || !offset || !mask || !grad_output || !grad_input || !grad_offset || !grad_mask ||
+        !grad_weight)
+        return fail(NLSPN_EINVAL, "null required pointer");
+    if (B < 1 || C < 1 || H < 1 || W < 1 || Cout < 1 || kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 ||
+        group < 1 || deformable_group < 1 || ph < 0 || pw < 0)
+        return fail(NLSPN_EINVAL, "invalid DCN arguments");
+    if ((C % group) != 0 || (Cout % group) != 0)
+        return fail(NLSPN_EINVAL, "channels(%d) and channels_out(%d) must divide group(%d)", C, Cout, group);
+    if ((C % deformable_group) != 0)
+        return fail(NLSPN_EINVAL, "channels(%d) must divide deformable_group(%d)", C, deformable_group);
+    const int Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1;
+    const int Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
+    if (Ho < 1 || Wo < 1) return fail(NLSPN_EINVAL, "output size %dx%d is empty", Ho, Wo);
+    hipStream_t s = as_stream(stream);
+    MdcnBwdArgs a{static_cast<const float *>(input), static_cast<const float *>(weight),
+                  static_cast<const float *>(offset), static_cast<const float *>(mask),
+                  static_cast<const float *>(grad_output), static_cast<float *>(grad_input),
+                  static_cast<float *>(grad_offset), static_cast<float *>(grad_mask), static_cast<float *>(grad_weight),
+                  static_cast<float *>(grad_bias), B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, group,
+                  deformable_group, Ho, Wo};
+    NLSPN_HIP_TRY(hipMemsetAsync(grad_input, 0, sizeof(float) * (size_t)B * C * H * W, s));
+    void *args[] = {&a};
+    const long long nd = (long long)B * deformable_group * kh * kw * Ho * Wo;
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel), dim3(elementwise_grid(nd)),
+                                  dim3(256), args, 0, s));
+    if (int rc = check_launch("nlspn_mdcn_backward data")) return rc;
+    const long long nw = (long long)Cout * (C / group) * kh * kw + (grad_bias ? Cout : 0);
+    if (nw > 0x7fffffffLL) return fail(NLSPN_EINVAL, "too many weight elements");
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_weight_kernel), dim3((unsigned)nw),
+                                  dim3(256), args, 0, s));
+    return check_launch("nlspn_mdcn_backward weight");
 }
 
 int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const void *dep, const void *aff,

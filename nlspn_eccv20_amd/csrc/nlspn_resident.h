@@ -116,21 +116,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RX = kResRX;
     constexpr unsigned ES = sizeof(T);
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    int *ctl = reinterpret_cast<int *>(smem);  // [0] abort, [1] min dep row, [2] max dep row
+    int *ctl = reinterpret_cast<int *>(smem);  // [0] abort, [1] / [2] row range scratch
     const int H = a.H, W = a.W, WW = W + 2 * RX, W4 = W / 4;
-    float *fwin = smem + 4;
-    float *cwin = fwin + (size_t)a.wh_max * WW;
-    float4 *akl = reinterpret_cast<float4 *>(cwin + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
+    float *fwin = smem + 4;                                                     // [wh_max][WW] f window
+    float4 *akl = reinterpret_cast<float4 *>(fwin + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
     const int NT = blockDim.x;
     const int tid = threadIdx.x, lane = tid & 63;
 
     const int b = blockIdx.x % a.B, j = blockIdx.x / a.B;
     const long long Q = (long long)H * W4;
     const long long qlo = (long long)j * Q / a.g, qhi = (long long)(j + 1) * Q / a.g;
-    const int rlo = (int)(qlo / W4) - RY, rhi = (int)((qhi - 1) / W4) + RY;  // window rows (inclusive)
-    const int WH = rhi - rlo + 1;
-    const int ra = rlo < 0 ? 0 : rlo, rb = rhi > H - 1 ? H - 1 : rhi;      // in-image window rows
-    const int nsq = (rb - ra + 1) * W4;                                    // staging quads per iteration
+    const int prow0 = (int)(qlo / W4), prow1 = (int)((qhi - 1) / W4);  // the part's own rows
 
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
@@ -175,41 +171,61 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         akl[K * NT + tid] = make_float4(aref[0], aref[1], aref[2], aref[3]);
     }
 
-    // ---- LDS init: f-window zero (cells outside the image stay 0 = zero padding),
-    // conf' window for the in-image cells (invariant), dependency rows
-    if (tid == 0) { ctl[0] = 0; ctl[1] = ra; ctl[2] = rb; }
-    for (int i = tid; i < WH * WW; i += NT) fwin[i] = 0.f;
-    if (has_conf) {
-        const rsrc_t rc = make_rsrc(static_cast<const T *>(a.conf) + b * HW);
-        for (int i = tid; i < nsq; i += NT) {
-            const int r = ra + i / W4, c = (i % W4) * 4;
-            float v[4];
-            ResVec<T>::template load<0>(rc, (unsigned)(r * W + c) * ES, 0u, v);
-            *reinterpret_cast<float4 *>(&cwin[(r - rlo) * WW + RX + c]) = make_float4(v[0], v[1], v[2], v[3]);
+    // ---- the window: every row a valid tap of this part touches (offsets are
+    // invariant, so once), when that span fits the LDS rows allocated; otherwise
+    // the part's rows +- RY, and the rare taps outside it take the general path.
+    if (tid == 0) { ctl[0] = 0; ctl[1] = prow0; ctl[2] = prow1; }  // own rows: the reference tap
+    __syncthreads();
+    const float Hf = (float)H, Wf = (float)W;
+    {
+        int mn = prow0, mx = prow1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // sample coordinates, .cuh:178-179
+                const float h_im = (float)(y - PH + i) + hy[k][e];
+                const float w_im = (float)(x0 + e - PW + jj) + hx[k][e];
+                hy[k][e] = h_im;
+                hx[k][e] = w_im;
+                if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                    const int h_low = (int)floorf(h_im);
+                    mn = min(mn, h_low);
+                    mx = max(mx, h_low + 1);
+                }
+            }
         }
+        if (active) { atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); }
     }
     __syncthreads();
-    // Classify every tap once (offsets are invariant):
+    int rlo = ctl[1], rhi = ctl[2];
+    if (rhi - rlo + 1 > a.wh_max) {  // span too tall for LDS: fixed halo + general path
+        rlo = prow0 - RY;
+        rhi = rlo + a.wh_max - 1;
+    }
+    const int WH = rhi - rlo + 1;
+    const int ra = rlo < 0 ? 0 : rlo, rb = rhi > H - 1 ? H - 1 : rhi;  // in-image window rows
+    const int nsq = (rb - ra + 1) * W4;                                // staging quads per iteration
+    __syncthreads();
+    if (tid == 0) { ctl[1] = ra; ctl[2] = rb; }
+    for (int i = tid; i < WH * WW; i += NT) fwin[i] = 0.f;  // cells outside the image stay 0
+    __syncthreads();
+    // Classify every tap once:
     //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
     //    coordinates are redirected to (rlo, -RX), an integer point of the window's
     //    zero padding columns, so the branch-free path reads four zeros with weights
     //    (1,0,0,0): v = +0 exactly, as the reference's val = 0;
     //  * in the LDS window: the branch-free path;
-    //  * valid but outside the window: read from global memory by the general path
-    //    (has_fb), and the dependency rows are widened to cover it.
-    const float Hf = (float)H, Wf = (float)W;
+    //  * valid but outside the window (only with a too-tall span): read from global
+    //    memory by the general path (has_fb); the dependency rows cover it.
     bool has_fb = false;
     {
         int mn = H, mx = -1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float h_im = (float)(y - PH + i) + hy[k][e];
-                const float w_im = (float)(x0 + e - PW + jj) + hx[k][e];
-                hy[k][e] = h_im;
-                hx[k][e] = w_im;
+                const float h_im = hy[k][e], w_im = hx[k][e];
                 if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                     const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
                     const int ry = h_low - rlo, rx = w_low + RX;
@@ -275,31 +291,34 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
         if (ctl[0]) return;
 
-        // ---- stage f = p_{t-1} * conf' for the in-image window cells (sc1 loads)
+        // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
+        // (written by other parts in this launch), conf' by plain loads (invariant)
         const T *p_in = p_all + (size_t)(t - 1) * N + b * HW;
         const rsrc_t rp = make_rsrc(p_in);
-        float sv[SMAX][4];
         const int nsq_it = (a.dbg & 2u) ? 0 : nsq;
+        for (int base = tb; base < nsq_it; base += SMAX * NT) {
+            float sv[SMAX][4], cv[SMAX][4];
 #pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-            const int i = tb + s * NT;
-            if (i < nsq_it) {
-                const int r = ra + i / W4, c = (i % W4) * 4;
-                ResVec<T>::template load<kSc1>(rp, (unsigned)(r * W + c) * ES, 0u, sv[s]);
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-            const int i = tb + s * NT;
-            if (i < nsq_it) {
-                const int r = ra + i / W4, c = (i % W4) * 4;
-                const int li = (r - rlo) * WW + RX + c;
-                float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
-                if (has_conf) {
-                    const float4 cc = *reinterpret_cast<const float4 *>(&cwin[li]);
-                    f.x = f.x * cc.x; f.y = f.y * cc.y; f.z = f.z * cc.z; f.w = f.w * cc.w;
+            for (int s = 0; s < SMAX; ++s) {
+                const int i = base + s * NT;
+                if (i < nsq_it) {
+                    const int r = ra + i / W4, c = (i % W4) * 4;
+                    const unsigned go = (unsigned)(r * W + c) * ES;
+                    ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
+                    if (has_conf) ResVec<T>::template load<0>(rcg, go, 0u, cv[s]);
                 }
-                *reinterpret_cast<float4 *>(&fwin[li]) = f;
+            }
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+                const int i = base + s * NT;
+                if (i < nsq_it) {
+                    const int r = ra + i / W4, c = (i % W4) * 4;
+                    float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
+                    if (has_conf) {
+                        f.x = f.x * cv[s][0]; f.y = f.y * cv[s][1]; f.z = f.z * cv[s][2]; f.w = f.w * cv[s][3];
+                    }
+                    *reinterpret_cast<float4 *>(&fwin[(r - rlo) * WW + RX + c]) = f;
+                }
             }
         }
         lds_barrier();

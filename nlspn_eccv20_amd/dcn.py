@@ -5,8 +5,7 @@ Reference: the pybind module `DCN` (src/model/deformconv/src/vision.cpp:6-13) wh
 src/model/modulated_deform_conv_func.py:13,26 (ModulatedDeformConvFunction).
 Installing this module as `DCN` (``sys.modules['DCN'] = nlspn_eccv20_amd.dcn``)
 lets the unmodified reference nlspnmodel.py run its offset branch on MI355X.
-Only the forward is native this round; the backward (vision.cpp:10) is the next
-row of the build plan and raises.
+Forward and backward (vision.cpp:9-10) are native HIP kernels (nlspn_mdcn.h).
 """
 from __future__ import annotations
 
@@ -61,9 +60,53 @@ def modulated_deform_conv_forward(input, weight, bias, offset, mask, kernel_h, k
     return out
 
 
-def modulated_deform_conv_backward(*args, **kwargs):
-    """vision.cpp:10 — not native yet (build plan §8f rank 1)."""
-    raise NotImplementedError("modulated_deform_conv_backward is not implemented on MI355X yet")
+def modulated_deform_conv_backward(input, weight, bias, offset, mask, grad_output, kernel_h, kernel_w, stride_h,
+                                   stride_w, pad_h, pad_w, dilation_h, dilation_w, group, deformable_group,
+                                   im2col_step):
+    """Same signature, checks and return list as modulated_deform_conv_cuda_backward
+    (modulated_deform_conv_cuda.cu:124-280): [grad_input, grad_offset, grad_mask,
+    grad_weight, grad_bias].  float32 (the reference also dispatches float64; the
+    MI355X build is float32).  Like the reference's col2im call (.cuh:371) grad_input
+    uses pad_h for the width padding too (identical for square padding)."""
+    if not input.is_contiguous():
+        raise RuntimeError("input tensor has to be contiguous")
+    if not weight.is_contiguous():
+        raise RuntimeError("weight tensor has to be contiguous")
+    for n, t in (("input", input), ("weight", weight), ("bias", bias), ("offset", offset), ("mask", mask),
+                 ("grad_output", grad_output)):
+        _cuda(n, t)
+    if input.dtype != torch.float32:
+        raise NotImplementedError("modulated_deform_conv_backward: float32 only on MI355X")
+    B, C, H, W = input.shape
+    Cout, Ckern, kh_, kw_ = weight.shape
+    if (C % group) != 0 or (Cout % group) != 0:
+        raise RuntimeError(f"channels({C}) and channels_out({Cout}) must divide group({group})")
+    if kh_ != kernel_h or kw_ != kernel_w:
+        raise RuntimeError(f"Input shape and kernel shape wont match: ({kernel_h} x {kernel_w} vs {kh_} x {kw_}).")
+    if C != Ckern * group:
+        raise RuntimeError(f"Input shape and kernel channels wont match: ({C} vs {Ckern * group}).")
+    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    if grad_output.shape[0] != B:
+        raise RuntimeError(f"Input shape and grad_out batch wont match: ({B} vs {grad_output.shape[0]}).")
+    if grad_output.shape[1] != Cout:
+        raise RuntimeError(f"Input shape and grad_out channels_out wont match: ({Cout} vs {grad_output.shape[1]}).")
+    if tuple(grad_output.shape[2:]) != (Ho, Wo):
+        raise RuntimeError(f"Input shape and grad_out shape wont match: ({Ho} x {Wo} vs "
+                           f"{grad_output.shape[2]} x {grad_output.shape[3]}).")
+    offset, mask, grad_output = offset.contiguous(), mask.contiguous(), grad_output.contiguous()
+    grad_input = torch.empty_like(input)
+    grad_offset = torch.empty_like(offset)
+    grad_mask = torch.empty_like(mask)
+    grad_weight = torch.empty_like(weight)
+    grad_bias = torch.empty_like(bias) if bias is not None else None
+    with torch.cuda.device(input.device):
+        _lib.check(_lib.get().nlspn_mdcn_backward(
+            _lib.DTYPE_F32, _ptr(input), _ptr(weight), _ptr(offset), _ptr(mask), _ptr(grad_output),
+            _ptr(grad_input), _ptr(grad_offset), _ptr(grad_mask), _ptr(grad_weight), _ptr(grad_bias),
+            B, C, H, W, Cout, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+            group, deformable_group, _stream(input.device)))
+    return [grad_input, grad_offset, grad_mask, grad_weight, grad_bias]
 
 
 class ModulatedDeformConvFunction(Function):
@@ -89,5 +132,10 @@ class ModulatedDeformConvFunction(Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, grad_output):
-        return modulated_deform_conv_backward()
+        input, offset, mask, weight, bias = ctx.saved_tensors
+        grad_input, grad_offset, grad_mask, grad_weight, grad_bias = modulated_deform_conv_backward(
+            input, weight, bias, offset, mask, grad_output, ctx.kernel_size[0], ctx.kernel_size[1], ctx.stride[0],
+            ctx.stride[1], ctx.padding[0], ctx.padding[1], ctx.dilation[0], ctx.dilation[1], ctx.groups,
+            ctx.deformable_groups, ctx.im2col_step)
+        return grad_input, grad_offset, grad_mask, grad_weight, grad_bias, None, None, None, None, None, None
 

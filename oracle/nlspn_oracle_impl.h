@@ -444,3 +444,176 @@ int FN(orc_propagate_backward)(const REAL *pred_init, const REAL *dep, const REA
     free(gaff); free(goff); free(gcf); free(gp); free(gf);
     return 0;
 }
+
+/* ---------------------------------------------------------------------------
+ * Generic modulated DCNv2 (seam 2 of the drop-in: the `DCN` module,
+ * src/model/deformconv/src/vision.cpp:9-10).  Any channels / groups /
+ * deformable groups / stride / padding / dilation.  Layouts as the reference:
+ *   input (B,C,H,W), weight (Cout, C/group, kh, kw), bias (Cout) or NULL,
+ *   offset (B, dg*2*kh*kw, Ho, Wo) [tap t: planes 2t (dh), 2t+1 (dw) of its group],
+ *   mask (B, dg*kh*kw, Ho, Wo), output (B, Cout, Ho, Wo).
+ * The sums the reference hands to BLAS (addmm / mm / addmv) are restated as plain
+ * sums in index order (BLAS order is unspecified; compared within tolerance).
+ * ------------------------------------------------------------------------- */
+
+/* im2col value (.cuh:127-194): val(b, c, t, ho, wo) * mask, with h_in/w_in from
+ * the given pads. */
+static REAL FN(orc_im2col_val)(const REAL *in, const REAL *off, const REAL *mask, int b, int c, int t,
+                               int ho, int wo, int C, int H, int W, int Ho, int Wo, int kw, int KK,
+                               int sh, int sw, int ph, int pw, int dh, int dw, int dg, int cpdg,
+                               REAL *inv_h_out, REAL *inv_w_out, REAL *m_out)
+{
+    const long long P = (long long)Ho * Wo, p = (long long)ho * Wo + wo;
+    const int dgi = c / cpdg, i = t / kw, j = t % kw;
+    const REAL oh = off[((long long)(b * dg + dgi) * 2 * KK + 2 * t) * P + p];
+    const REAL ow = off[((long long)(b * dg + dgi) * 2 * KK + 2 * t + 1) * P + p];
+    const REAL m = mask[((long long)(b * dg + dgi) * KK + t) * P + p];
+    const REAL h_im = (ho * sh - ph + i * dh) + oh;  /* int + int, then + offset (.cuh:178-179) */
+    const REAL w_im = (wo * sw - pw + j * dw) + ow;
+    REAL val = 0;
+    if (h_im > -1 && w_im > -1 && h_im < H && w_im < W)
+        val = FN(orc_bilinear)(in + ((long long)b * C + c) * H * W, H, W, h_im, w_im);
+    if (inv_h_out) *inv_h_out = h_im;
+    if (inv_w_out) *inv_w_out = w_im;
+    if (m_out) *m_out = m;
+    return val * m;
+}
+
+/* forward: im2col + per-group addmm(bias, columns^T, weight^T) (.cu:90-116) */
+void FN(orc_mdcn_fwd)(const REAL *in, const REAL *wt, const REAL *bias, const REAL *off, const REAL *mask,
+                      int B, int C, int H, int W, int Cout, int kh, int kw, int sh, int sw, int ph, int pw,
+                      int dh, int dw, int group, int dg, REAL *out)
+{
+    const int Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1, Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
+    const int KK = kh * kw, cpg = C / group, opg = Cout / group, cpdg = C / dg;
+    const long long P = (long long)Ho * Wo;
+#pragma omp parallel for collapse(2) num_threads(orc_threads) schedule(static)
+    for (int b = 0; b < B; ++b)
+        for (int co = 0; co < Cout; ++co) {
+            const int g = co / opg;
+            for (long long p = 0; p < P; ++p) {
+                const int ho = (int)(p / Wo), wo = (int)(p % Wo);
+                REAL acc = 0;
+                for (int cl = 0; cl < cpg; ++cl)
+                    for (int t = 0; t < KK; ++t) {
+                        const REAL col = FN(orc_im2col_val)(in, off, mask, b, g * cpg + cl, t, ho, wo, C, H, W, Ho, Wo,
+                                                            kw, KK, sh, sw, ph, pw, dh, dw, dg, cpdg, 0, 0, 0);
+                        acc += col * wt[((long long)co * cpg + cl) * KK + t];
+                    }
+                out[((long long)b * Cout + co) * P + p] = bias ? acc + bias[co] : acc;
+            }
+        }
+}
+
+/* mdmcn_get_gradient_weight (.cuh:57-81) */
+static REAL FN(orc_grad_weight)(REAL ah, REAL aw, int h, int w, int H, int W)
+{
+    if (ah <= -1 || ah >= H || aw <= -1 || aw >= W) return 0;
+    const int hl = (int)FLOOR(ah), wl = (int)FLOOR(aw), hh = hl + 1, wh = wl + 1;
+    REAL weight = 0;
+    if (h == hl && w == wl) weight = (h + 1 - ah) * (w + 1 - aw);
+    if (h == hl && w == wh) weight = (h + 1 - ah) * (aw + 1 - w);
+    if (h == hh && w == wl) weight = (ah + 1 - h) * (w + 1 - aw);
+    if (h == hh && w == wh) weight = (ah + 1 - h) * (aw + 1 - w);
+    return weight;
+}
+
+/* backward (.cu:124-280): columns = weight_g^T . grad_output_g per group; then
+ * col2im_coord (.cuh:256-328) -> grad_offset, grad_mask; col2im (.cuh:196-254) ->
+ * grad_input, with the reference's pad_w := pad_h at its call site (.cuh:371);
+ * im2col again -> grad_weight += grad_output_g . columns_g^T; grad_bias +=
+ * grad_output_g . ones.  grad_bias may be NULL.  Returns 0, or -1 on allocation
+ * failure. */
+int FN(orc_mdcn_bwd)(const REAL *in, const REAL *wt, const REAL *off, const REAL *mask, const REAL *go,
+                     int B, int C, int H, int W, int Cout, int kh, int kw, int sh, int sw, int ph, int pw,
+                     int dh, int dw, int group, int dg, REAL *g_in, REAL *g_off, REAL *g_mask, REAL *g_wt,
+                     REAL *g_bias)
+{
+    const int Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1, Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
+    const int KK = kh * kw, cpg = C / group, opg = Cout / group, cpdg = C / dg;
+    const long long P = (long long)Ho * Wo, BP = (long long)B * P, HW = (long long)H * W;
+    REAL *col = (REAL *)malloc(sizeof(REAL) * (size_t)C * KK * (size_t)BP);
+    if (!col) return -1;
+    /* columns (.cu:213-220) */
+    for (int c = 0; c < C; ++c) {
+        const int g = c / cpg, cl = c % cpg;
+        for (int t = 0; t < KK; ++t)
+            for (int b = 0; b < B; ++b)
+                for (long long p = 0; p < P; ++p) {
+                    REAL s = 0;
+                    for (int ol = 0; ol < opg; ++ol) {
+                        const int co = g * opg + ol;
+                        s += wt[((long long)co * cpg + cl) * KK + t] * go[((long long)b * Cout + co) * P + p];
+                    }
+                    col[((long long)c * KK + t) * BP + (long long)b * P + p] = s;
+                }
+    }
+    /* col2im_coord (.cuh:256-328) */
+    for (int b = 0; b < B; ++b)
+        for (int dgi = 0; dgi < dg; ++dgi)
+            for (int oc = 0; oc < 2 * KK; ++oc)
+                for (long long p = 0; p < P; ++p) {
+                    const int t = oc / 2, dir = oc % 2, ho = (int)(p / Wo), wo = (int)(p % Wo);
+                    REAL val = 0, mval = 0;
+                    for (int cnt = 0; cnt < cpdg; ++cnt) {
+                        const int c = dgi * cpdg + cnt;
+                        const REAL cv = col[((long long)c * KK + t) * BP + (long long)b * P + p];
+                        REAL ih, iw, m;
+                        FN(orc_im2col_val)(in, off, mask, b, c, t, ho, wo, C, H, W, Ho, Wo, kw, KK, sh, sw, ph, pw,
+                                           dh, dw, dg, cpdg, &ih, &iw, &m);
+                        const REAL *im = in + ((long long)b * C + c) * HW;
+                        if (ih <= -1 || iw <= -1 || ih >= H || iw >= W) {
+                            ih = iw = -2;
+                        } else {
+                            mval += cv * FN(orc_bilinear)(im, H, W, ih, iw);
+                        }
+                        const REAL weight = FN(orc_coord_weight)(ih, iw, H, W, im, dir);
+                        val += weight * cv * m;
+                    }
+                    g_off[((long long)(b * dg + dgi) * 2 * KK + oc) * P + p] = val;
+                    if (dir == 0) g_mask[((long long)(b * dg + dgi) * KK + t) * P + p] = mval;
+                }
+    /* col2im (.cuh:196-254), pad_w := pad_h as the reference's call passes it */
+    memset(g_in, 0, sizeof(REAL) * (size_t)B * C * HW);
+    for (int c = 0; c < C; ++c)
+        for (int t = 0; t < KK; ++t)
+            for (int b = 0; b < B; ++b)
+                for (long long p = 0; p < P; ++p) {
+                    const int ho = (int)(p / Wo), wo = (int)(p % Wo);
+                    REAL ih, iw, m;
+                    FN(orc_im2col_val)(in, off, mask, b, c, t, ho, wo, C, H, W, Ho, Wo, kw, KK, sh, sw, ph, ph, dh,
+                                       dw, dg, cpdg, &ih, &iw, &m);
+                    const REAL top = col[((long long)c * KK + t) * BP + (long long)b * P + p] * m;
+                    const int ch = (int)ih, cw = (int)iw;
+                    for (int dy = -2; dy <= 2; ++dy)
+                        for (int dx = -2; dx <= 2; ++dx) {
+                            const int y = ch + dy, x = cw + dx;
+                            if (y >= 0 && y < H && x >= 0 && x < W && FABS(ih - y) < 1 && FABS(iw - x) < 1) {
+                                const REAL weight = FN(orc_grad_weight)(ih, iw, y, x, H, W);
+                                g_in[((long long)b * C + c) * HW + (long long)y * W + x] += weight * top;
+                            }
+                        }
+                }
+    /* grad_weight / grad_bias (.cu:262-273) */
+    for (int co = 0; co < Cout; ++co) {
+        const int g = co / opg;
+        for (int cl = 0; cl < cpg; ++cl)
+            for (int t = 0; t < KK; ++t) {
+                REAL s = 0;
+                for (int b = 0; b < B; ++b)
+                    for (long long p = 0; p < P; ++p)
+                        s += go[((long long)b * Cout + co) * P + p] *
+                             FN(orc_im2col_val)(in, off, mask, b, g * cpg + cl, t, (int)(p / Wo), (int)(p % Wo), C, H,
+                                                W, Ho, Wo, kw, KK, sh, sw, ph, pw, dh, dw, dg, cpdg, 0, 0, 0);
+                g_wt[((long long)co * cpg + cl) * KK + t] = s;
+            }
+        if (g_bias) {
+            REAL s = 0;
+            for (int b = 0; b < B; ++b)
+                for (long long p = 0; p < P; ++p) s += go[((long long)b * Cout + co) * P + p];
+            g_bias[co] = s;
+        }
+    }
+    free(col);
+    return 0;
+}

@@ -174,3 +174,43 @@ def propagate_backward(pred_init, dep, conf, aff_raw, off_raw, gamma, grad_pred,
         raise ValueError(f"oracle backward rejected its arguments (code {rc})")
     return {"pred_init": g_pi, "confidence": g_conf if conf is not None else None, "aff": g_aff,
             "offset": g_off, "gamma": float(g_gamma[0])}
+
+
+def _mdcn_shape(H, W, kh, kw, sh, sw, ph, pw, dh, dw):
+    return (H + 2 * ph - (dh * (kh - 1) + 1)) // sh + 1, (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
+
+
+def mdcn_forward(inp, weight, bias, offset, mask, stride=(1, 1), padding=(1, 1), dilation=(1, 1), group=1,
+                 deformable_group=1):
+    """Generic modulated DCNv2 forward (seam 2, vision.cpp:9): .cuh:127-194 + .cu:90-116."""
+    dtype = inp.dtype
+    sfx, _ = _sfx(dtype)
+    inp, weight, offset, mask = (_c(x, dtype) for x in (inp, weight, offset, mask))
+    bias = _c(bias, dtype)
+    B, C, H, W = inp.shape
+    Cout, _, kh, kw = weight.shape
+    Ho, Wo = _mdcn_shape(H, W, kh, kw, *stride, *padding, *dilation)
+    out = np.empty((B, Cout, Ho, Wo), dtype=dtype)
+    getattr(lib(), f"orc_mdcn_fwd_{sfx}")(_p(inp), _p(weight), _p(bias), _p(offset), _p(mask), B, C, H, W, Cout, kh,
+                                          kw, *stride, *padding, *dilation, group, deformable_group, _p(out))
+    return out
+
+
+def mdcn_backward(inp, weight, offset, mask, grad_output, stride=(1, 1), padding=(1, 1), dilation=(1, 1),
+                  group=1, deformable_group=1, with_bias=True):
+    """Generic modulated DCNv2 backward (seam 2, vision.cpp:10; .cu:124-280), including the
+    reference's pad_w := pad_h in its col2im call (.cuh:371).  Returns
+    (grad_input, grad_offset, grad_mask, grad_weight, grad_bias or None)."""
+    dtype = inp.dtype
+    sfx, _ = _sfx(dtype)
+    inp, weight, offset, mask, grad_output = (_c(x, dtype) for x in (inp, weight, offset, mask, grad_output))
+    B, C, H, W = inp.shape
+    Cout, _, kh, kw = weight.shape
+    gi, goff, gm, gw = (np.empty_like(x) for x in (inp, offset, mask, weight))
+    gb = np.empty((Cout,), dtype=dtype) if with_bias else None
+    rc = getattr(lib(), f"orc_mdcn_bwd_{sfx}")(
+        _p(inp), _p(weight), _p(offset), _p(mask), _p(grad_output), B, C, H, W, Cout, kh, kw, *stride, *padding,
+        *dilation, group, deformable_group, _p(gi), _p(goff), _p(gm), _p(gw), _p(gb))
+    if rc != 0:
+        raise MemoryError("oracle mdcn backward: allocation failed")
+    return gi, goff, gm, gw, gb

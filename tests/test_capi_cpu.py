@@ -77,6 +77,12 @@ def test_propagate_validation():
     assert rc == _lib.EINVAL and "affinity kind" in lib.nlspn_last_error().decode()
     rc = lib.nlspn_mdcn_forward(0, p, p, None, p, p, p, 1, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 2, 1, None)
     assert rc == _lib.EINVAL and "must divide group" in lib.nlspn_last_error().decode()
+    rc = lib.nlspn_mdcn_backward(0, p, p, p, p, p, p, p, p, p, None, 1, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 2, 1,
+                                 None)
+    assert rc == _lib.EINVAL and "must divide group" in lib.nlspn_last_error().decode()
+    rc = lib.nlspn_mdcn_backward(1, p, p, p, p, p, p, p, p, p, None, 1, 4, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 2, 1,
+                                 None)
+    assert rc == _lib.EUNSUPPORTED and "float32" in lib.nlspn_last_error().decode()
 
 
 def test_host_requires_cuda_tensors():

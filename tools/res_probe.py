@@ -26,6 +26,7 @@ def run(B=8, H=228, W=304, T=18, reps=20, dbgs=(0, 1, 2, 4, 3, 6, 7), resident=(
     o = _alloc_outputs(pi, 8, T, True, True)
     lib = _lib.get()
     grid = ctypes.c_int()
+    os.environ["NLSPN_RESIDENT"] = "1"
     lib.nlspn_resident_config(0, B, H, W, 3, 3, T, 1, ctypes.byref(grid), None, None)
     res = []
     for r in resident:
