@@ -14,10 +14,13 @@ Multi-GPU (torchrun): every rank runs its own batch (weak scaling, no collective
 on the data path) — the all_reduce below only takes the max time.
 
 Extra JSON objects:
-  roofline     — the fused iteration kernel: algorithmic bytes per launch
-                 (S*(4+3K) per pixel) / mean kernel duration from
-                 dispatch-recorded HIP events (nlspn_time_prop_step) on this
-                 stream; traffic from profiles/pmc_<config>.json when present.
+  roofline     — the dominant kernel: the resident kernel (iterations 2..T in
+                 one launch) where it applies, else the per-iteration step kernel.
+                 achieved = algorithmic bytes per launch (S*(4+3K) per
+                 pixel-iteration, SURVEY §8(d), x the pixel-iterations one launch
+                 processes) / its mean duration from dispatch-recorded HIP events
+                 (nlspn_time_propagate) on this stream; traffic = HBM bytes per
+                 launch from profiles/pmc_<config>.json (rocprofv3 PMC) when present.
   backward     — (fp32 configs) forward+backward of the section through autograd
                  (nlspn_propagate + nlspn_propagate_backward), ms per step and per
                  iteration, HIP-event timed on this stream; not part of `value`.
@@ -70,7 +73,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="nyu", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel-reps", type=int, default=200)
+    ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-backward", action="store_true")
@@ -79,20 +82,37 @@ def parse():
 
 
 def kernel_time(plan, inputs, cfg, reps, dev):
-    """Mean/min duration of the fused iteration kernel from dispatch-recorded events."""
+    """Dispatch-recorded HIP-event durations (nlspn_time_propagate) on this stream, over
+    `reps` whole propagations on the plan's buffers: step 1 (prologue fused) and
+    iterations 2..T — one resident-kernel launch, or the sum of the T-1 step kernels."""
     o = plan.outputs
     K = cfg["kernel"][0] * cfg["kernel"][1] - 1
-    off = inputs["off"]
-    p_out = torch.empty_like(o["pred"])
-    H, W, B = cfg["H"], cfg["W"], cfg["B"]
-    mean_ms, min_ms = ctypes.c_float(), ctypes.c_float()
+    aff, off = inputs["aff"], inputs["off"]
+    first, rest, res = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
     dt = _lib.DTYPE_F16 if cfg["dtype"] == "f16" else _lib.DTYPE_F32
-    _lib.check(_lib.get().nlspn_time_prop_step(
-        dt, _ptr(o["pred_inter"][0]), _ptr(o["confidence"]), _ptr(inputs["dep"]), _ptr(o["aff"]),
-        (K + 1) * H * W, _ptr(off), off.stride(0), _lib.OFF_RAW, _ptr(p_out), B, H, W,
-        cfg["kernel"][0], cfg["kernel"][1], _lib.PRESERVE_INPUT, reps, _stream(dev),
-        ctypes.byref(mean_ms), ctypes.byref(min_ms)))
-    return mean_ms.value, min_ms.value
+    _lib.check(_lib.get().nlspn_time_propagate(
+        dt, _ptr(inputs["pred_init"]), _ptr(inputs["dep"]), _ptr(inputs["conf"]), _ptr(aff), aff.stride(0),
+        _ptr(off), off.stride(0), _ptr(inputs["gamma"]), _ptr(o["pred_inter"]), _ptr(o["pred"]), _ptr(o["aff"]),
+        _ptr(o["offset"]), _ptr(o["confidence"]), _ptr(o["workspace"]), cfg["B"], cfg["H"], cfg["W"],
+        cfg["kernel"][0], cfg["kernel"][1], cfg["T"], _lib.AFF_KINDS["TGASS"], _lib.PRESERVE_INPUT, reps,
+        _stream(dev), ctypes.byref(first), ctypes.byref(rest), ctypes.byref(res)))
+    assert K == aff.shape[1]
+    return first.value, rest.value, bool(res.value)
+
+
+def pmc_traffic(config, kernel):
+    """HBM-side bytes per launch of `kernel` from profiles/pmc_<config>.json (rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    entries = d.get("kernels", {d.get("kernel", ""): d})
+    for name, e in entries.items():
+        if kernel in name:
+            return e.get("hbm_bytes_per_launch")
+    return None
 
 
 def backward_timing(inputs, cfg, steps):
@@ -196,17 +216,18 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
     elapsed = max_over_ranks(elapsed, dev)
 
-    kmean, kmin = kernel_time(plan, inputs, cfg, a.kernel_reps, dev)
+    first_ms, rest_ms, resident = kernel_time(plan, inputs, cfg, a.kernel_reps, dev)
     npx = cfg["B"] * cfg["H"] * cfg["W"]
     es = 2 if cfg["dtype"] == "f16" else 4
-    bytes_per_launch = es * (4 + 3 * K) * npx
+    # S*(4+3K) algorithmic bytes per pixel-iteration.  The dominant
+    # kernel is the resident kernel (T-1 pixel-iterations per pixel in one launch)
+    # when it applies, else the per-iteration step kernel (one per launch).
+    iters = cfg["T"] - 1 if resident else 1
+    kname = "prop_resident_kernel" if resident else "prop_step_kernel"
+    kmean = rest_ms if resident else rest_ms / max(1, cfg["T"] - 1)
+    bytes_per_launch = es * (4 + 3 * K) * npx * iters
     achieved = bytes_per_launch / (kmean * 1e-3) / 1e9
-
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic = pmc_traffic(a.config, kname)
 
     ms_per_step = 1e3 * elapsed / a.steps
     value = world * cfg["T"] * a.steps / elapsed
@@ -222,9 +243,11 @@ def main():
                    "parallelism": f"dp{world} (batch shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "prop_step_kernel (one fused iteration)",
+                     "kernel": (f"{kname} (iterations 2..{cfg['T']} in one launch, invariant planes on chip)"
+                                if resident else f"{kname} (one fused iteration)"),
+                     "pixel_iterations_per_launch": npx * iters,
                      "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "kernel_ms_mean": round(kmean, 5), "kernel_ms_min": round(kmin, 5)},
+                     "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5)},
         "gpu_event_ms_per_step": round(gpu_ms / a.steps, 4),
     }
     if cfg["dtype"] == "f32" and not a.no_backward:

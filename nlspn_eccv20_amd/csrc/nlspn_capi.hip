@@ -152,7 +152,8 @@ int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = null
 // Iterations 2..T in one launch with the invariant planes held on chip
 // (nlspn_resident.h).  Applies to the 3x3 learned-offset geometry when every
 // part's quads fit one workgroup and its window fits LDS; otherwise the T-1
-// per-iteration launches run.  Opt-in (NLSPN_RESIDENT=1) for now.
+// per-iteration launches run.  NLSPN_RESIDENT=0 in the environment forces the
+// per-iteration launches (A/B measurement).
 constexpr int kResMaxNT = 768;
 constexpr size_t kSyncBytes = 4096;  // progress words + abort word (nlspn_workspace_bytes)
 
@@ -177,7 +178,7 @@ struct ResPlan {
 
 template <typename T>
 const void *res_fn() {
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 4>);
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2>);
 }
 
 // Fills P and returns true when the resident kernel applies.
@@ -185,7 +186,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
                    int kw, int T, unsigned flags, ResPlan &P) {
     const char *env = getenv("NLSPN_RESIDENT");
-    if (!env || env[0] != '1') return false;  // opt-in while it trails the per-iteration launches at C2
+    if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
     const size_t es = esize(dtype), vb = 4 * es;
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
@@ -213,11 +214,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
         nt = (qmax + 63) / 64 * 64;
         if (nt > kResMaxNT) break;  // fewer parts only makes them larger
         const long long avail = (long long)kLdsBytes - 16 - 16LL * 9 * nt;
-        wh_max = avail > 0 ? avail / WWb : 0;
+        wh_max = avail > 0 ? avail / (2 * WWb) : 0;  // two copies of the window
         if (wh_max >= rows_max + 2 * kResRY) break;
     }
     if (g < 1 || nt > kResMaxNT || wh_max < 1) return false;
-    const size_t lds = 16 + (size_t)(wh_max * WWb) + 16 * 9 * (size_t)nt;
+    const size_t lds = 16 + (size_t)(2 * wh_max * WWb) + 16 * 9 * (size_t)nt;
     if (lds > kLdsBytes || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
     const unsigned G = (unsigned)(B * g);
     if ((G + 1) * 4 > kSyncBytes) return false;

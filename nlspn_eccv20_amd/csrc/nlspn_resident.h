@@ -118,8 +118,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int *ctl = reinterpret_cast<int *>(smem);  // [0] abort, [1] / [2] row range scratch
     const int H = a.H, W = a.W, WW = W + 2 * RX, W4 = W / 4;
-    float *fwin = smem + 4;                                                     // [wh_max][WW] f window
-    float4 *akl = reinterpret_cast<float4 *>(fwin + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
+    // f window twice: fwin[i] and fwinB[i] = fwin[i + 1], so any horizontal pair
+    // (s[rx], s[rx+1]) is ONE 8-byte-aligned ds_read_b64 from one of the copies
+    float *fwin = smem + 4;                                                      // [wh_max][WW]
+    float *fwinB = fwin + (size_t)a.wh_max * WW;                                 // [wh_max][WW], shifted by 1
+    float4 *akl = reinterpret_cast<float4 *>(fwinB + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
     const int NT = blockDim.x;
     const int tid = threadIdx.x, lane = tid & 63;
 
@@ -208,7 +211,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int nsq = (rb - ra + 1) * W4;                                // staging quads per iteration
     __syncthreads();
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; }
-    for (int i = tid; i < WH * WW; i += NT) fwin[i] = 0.f;  // cells outside the image stay 0
+    for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     __syncthreads();
     // Classify every tap once:
     //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
@@ -247,6 +250,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int jlo = res_owner((long long)ctl[1] * W4, Q, a.g);
     const int jhi = res_owner((long long)(ctl[2] + 1) * W4 - 1, Q, a.g);
     const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
+    const float WWf = (float)WW;
+    const int lbase = RX - rlo * WW;
 
     const T *p_all = static_cast<const T *>(a.pred_inter);
     T *p_out_all = static_cast<T *>(a.pred_inter);
@@ -317,7 +322,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     if (has_conf) {
                         f.x = f.x * cv[s][0]; f.y = f.y * cv[s][1]; f.z = f.z * cv[s][2]; f.w = f.w * cv[s][3];
                     }
-                    *reinterpret_cast<float4 *>(&fwin[(r - rlo) * WW + RX + c]) = f;
+                    const int li = (r - rlo) * WW + RX + c;  // li % 4 == 0
+                    *reinterpret_cast<float4 *>(&fwin[li]) = f;
+                    fwinB[li - 1] = f.x;
+                    *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
+                    fwinB[li + 2] = f.w;
                 }
             }
         }
@@ -343,8 +352,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     const float lh = h_im - fh, lw = w_im - fw;  // = h - (float)h_low (.cuh:35-36)
                     const float hh = 1.f - lh, hw = 1.f - lw;
                     const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    const float *sp = &fwin[((int)fh - rlo) * WW + (int)fw + RX];
-                    const float v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
+                    // window index (h_low - rlo) * WW + w_low + RX, in exact float arithmetic
+                    const int li = (int)(fh * WWf + fw) + lbase;
+                    const int par = li & 1;
+                    const float2 *sp = reinterpret_cast<const float2 *>((par ? fwinB : fwin) + (li - par));
+                    const float2 s01 = sp[0], s23 = sp[WW / 2];
+                    const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                     acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
                 }
             }
