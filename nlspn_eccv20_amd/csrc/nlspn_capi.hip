@@ -233,9 +233,9 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     return true;
 }
 
+// The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words).
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
-    NLSPN_HIP_TRY(hipMemsetAsync(P.a.sync, 0, P.sync_bytes, s));
     void *args[] = {&P.a};
     if (e0)
         NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s, e0, e1, 0));
@@ -360,10 +360,15 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
     if (T > 1 && (rc = prepare_step(r, L))) return rc;
 
     if (resident) *resident = 0;
-    if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
     ResPlan P;
-    if (plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter, pred,
-                      workspace, B, H, W, kh, kw, T, flags, P)) {
+    const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
+                                   pred, workspace, B, H, W, kh, kw, T, flags, P);
+    if (res) {  // step 1 zeroes the resident kernel's progress words
+        r1.a.zero_words = P.a.sync;
+        r1.a.nzero = (int)(P.sync_bytes / 4);
+    }
+    if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
+    if (res) {
         if (resident) *resident = 1;
         return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
     }

@@ -59,6 +59,8 @@ struct StepArgs {
     void *off_out;       // 2(K+1) planes per item, contiguous, or null
     void *conf_out;      // B planes, or null iff conf null
     int kind;            // affinity kind
+    unsigned *zero_words;  // FIRST: progress words of the resident kernel that follows, zeroed here
+    int nzero;             //   (replaces a memset node; the kernel boundary orders it)
 };
 
 constexpr unsigned kPreserve = 0x1u;
@@ -132,6 +134,9 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     const int x0 = tx * TW, y0 = ty * TH;
     const int wy0 = y0 - RY, wx0 = x0 - RX;
 
+    if (FIRST && a.zero_words && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < a.nzero; i += NT)
+            __hip_atomic_store(a.zero_words + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
