@@ -67,6 +67,11 @@ struct ResArgs {
 
 constexpr int kResRY = 8, kResRX = 8;            // window halo (rows, columns)
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
+#ifndef NLSPN_RES_NOGP
+constexpr bool kResGeneralPath = true;
+#else
+constexpr bool kResGeneralPath = false;  // experiment only: wrong results for taps outside the window
+#endif
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 
 // Part j of an image with Q quads owns quads [j*Q/g, (j+1)*Q/g); owner(q) is the
@@ -365,7 +370,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // reference's per-corner checks, from global memory where needed.  It
             // re-reads its offsets from global memory and runs a rolled tap loop, so it
             // shares no registers with the branch-free path (no spills around it).
-            if (wave_fb && has_fb) {
+            if (kResGeneralPath && wave_fb && has_fb) {
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
