@@ -24,6 +24,8 @@ Extra JSON objects:
   backward     — (fp32 configs) forward+backward of the section through autograd
                  (nlspn_propagate + nlspn_propagate_backward), ms per step and per
                  iteration, HIP-event timed on this stream; not part of `value`.
+  gru_section  — (fp32, 3x3) the GRU-mode section (the reference's default), eager
+                 vs one hipGraph (SectionGraph); not part of `value`.
   cpu_baseline — the C oracle (kind "port"; the reference has no CPU DCN path)
                  on the same workload, rank 0, N=1.
 """
@@ -77,6 +79,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-backward", action="store_true")
+    ap.add_argument("--no-gru", action="store_true")
     ap.add_argument("--backward-steps", type=int, default=20)
     return ap.parse_args()
 
@@ -151,6 +154,47 @@ def backward_timing(inputs, cfg, steps):
     return {"ms_fwd_bwd_per_step": round(fb, 4), "ms_fwd_per_step": round(fo, 4),
             "ms_bwd_per_iter": round((fb - fo) / cfg["T"], 5), "steps": steps,
             "note": "eager autograd (not graph-replayed); bwd = fwd+bwd - fwd"}
+
+
+def gru_section_timing(inputs, cfg, steps, dev):
+    """GRU mode (the reference's forced default, src/config.py:225-228): the section of
+    NLSPNModel (nlspnmodel.py:303-383, ConvGRU re-estimating the affinity every
+    iteration) on the bench's synthetic head outputs, random-init GRU weights, eager
+    vs captured into one hipGraph (SectionGraph).  Not part of `value`."""
+    import types
+    from nlspn_eccv20_amd import NLSPNModel, SectionGraph
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    args = types.SimpleNamespace(prop_kernel=cfg["kernel"][0], affinity="TGASS", affinity_gamma=0.5,
+                                 prop_time=cfg["T"], preserve_input=True, always_clip=False, conf_prop=True,
+                                 offset=True, network="resnet34", from_scratch=True, zero_init_aff=False,
+                                 use_GRU=True, use_S2D=False, GRU_hidden_dim=128, GRU_input_dim=128, lr=1e-3,
+                                 max_depth=cfg["max_depth"], patch_height=cfg["H"], patch_width=cfg["W"],
+                                 model_name="NLSPN")
+    torch.manual_seed(0)
+    m = NLSPNModel(args).to(dev).eval()
+    off_aff = torch.cat([inputs["off"], inputs["aff"]], 1).contiguous()
+    heads = (inputs["pred_init"], off_aff, inputs["conf"], inputs["dep"])
+    assert off_aff.shape[1] == 3 * K
+    g = SectionGraph(m, *heads)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    with torch.no_grad():
+        for _ in range(3):
+            m.propagate_heads(*heads)
+            g.replay()
+        torch.cuda.synchronize()
+        e[0].record()
+        for _ in range(steps):
+            m.propagate_heads(*heads)
+        e[1].record()
+        e[2].record()
+        for _ in range(steps):
+            g.replay()
+        e[3].record()
+    torch.cuda.synchronize()
+    eager, graph = e[0].elapsed_time(e[1]) / steps, e[2].elapsed_time(e[3]) / steps
+    return {"ms_per_step_eager": round(eager, 4), "ms_per_step_graph": round(graph, 4),
+            "iters_per_s_graph": round(cfg["T"] / (graph * 1e-3), 1), "steps": steps,
+            "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration"}
 
 
 def cpu_baseline(cfg, s, reps):
@@ -252,6 +296,8 @@ def main():
     }
     if cfg["dtype"] == "f32" and not a.no_backward:
         out["backward"] = backward_timing(inputs, cfg, a.backward_steps)
+    if cfg["dtype"] == "f32" and cfg["kernel"] == (3, 3) and not a.no_gru:
+        out["gru_section"] = gru_section_timing(inputs, cfg, a.backward_steps, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, s, a.cpu_reps)
     plan.close()

@@ -9,11 +9,12 @@ with a torch-facing mirror of the reference interface:
   propagation.NLSPNPropagation  — nn.Module with the reference's state_dict names
   dcn                           — `DCN`-compatible module (seam 2)
   model.NLSPNModel              — the whole reference model (seam 1), heads on MIOpen
+  model.SectionGraph            — its propagation section (GRU mode included) as one hipGraph
 """
-from .model import NLSPNModel
+from .model import NLSPNModel, SectionGraph
 from .propagation import (NLSPNPropagation, PropagationPlan, affinity_normalization, kernel_geometry,
                           off_insert, prop_step, propagate)
 
-__all__ = ["NLSPNModel", "NLSPNPropagation", "PropagationPlan", "affinity_normalization", "kernel_geometry", "off_insert",
+__all__ = ["NLSPNModel", "NLSPNPropagation", "PropagationPlan", "SectionGraph", "affinity_normalization", "kernel_geometry", "off_insert",
            "prop_step", "propagate"]
 __version__ = "0.1.0"

@@ -211,3 +211,28 @@ def test_model_nyu_size_gru():
         out = m(s)
     assert out["pred"].shape == (2, 1, 228, 304) and torch.isfinite(out["pred"]).all()
     assert (out["pred"] >= 0).all() and len(out["pred_inter"]) == 18
+
+
+@pytest.mark.parametrize("use_gru", [True, False])
+def test_section_graph_equals_eager(use_gru):
+    """SectionGraph (the section captured into one hipGraph, GRU convolutions included)
+    replays exactly what the eager section computes, and picks up new head outputs."""
+    from nlspn_eccv20_amd import SectionGraph
+    torch.manual_seed(0)
+    m = NLSPNModel(make_args(use_GRU=use_gru, prop_time=6, patch_height=48, patch_width=80)).to(DEV).eval()
+    randomize_aff_head(m)
+    s1, s2 = sample(2, 48, 80, seed=3), sample(2, 48, 80, seed=4)
+    with torch.no_grad():
+        h1, h2 = m.heads(s1), m.heads(s2)
+        g = SectionGraph(m, *h1, s1["dep"])
+        for h, smp in ((h1, s1), (h2, s2), (h1, s1)):
+            eager = m.propagate_heads(*h, smp["dep"])
+            o = g.replay(*h, smp["dep"])
+            torch.cuda.synchronize()
+            if use_gru:  # MIOpen may choose another conv algorithm per call: rounding-level only
+                for a, b in zip(o["pred_inter"] + [o["pred"]], eager["pred_inter"] + [eager["pred"]]):
+                    assert ((a - b).norm() / b.norm()).item() <= 1e-5
+            else:
+                assert torch.equal(o["pred"], eager["pred"])
+                for a, b in zip(o["pred_inter"], eager["pred_inter"]):
+                    assert torch.equal(a, b)
