@@ -19,6 +19,12 @@
 #include "nlspn_step.h"
 #include "nlspn_resident.h"
 
+// defined in nlspn_kern_resident.hip (own translation unit and flags)
+namespace nlspn {
+extern template __global__ void prop_resident_kernel<float, kResMaxNT, 2>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, kResMaxNT, 2>(ResArgs);
+}  // namespace nlspn
+
 using namespace nlspn;
 
 namespace {
@@ -154,7 +160,6 @@ int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = null
 // part's quads fit one workgroup and its window fits LDS; otherwise the T-1
 // per-iteration launches run.  NLSPN_RESIDENT=0 in the environment forces the
 // per-iteration launches (A/B measurement).
-constexpr int kResMaxNT = 768;
 constexpr size_t kSyncBytes = 4096;  // progress words + abort word (nlspn_workspace_bytes)
 
 int device_cus() {

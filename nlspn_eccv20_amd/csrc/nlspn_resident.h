@@ -65,6 +65,7 @@ struct ResArgs {
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps
 };
 
+constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
 constexpr int kResRY = 8, kResRX = 8;            // window halo (rows, columns)
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
 #ifndef NLSPN_RES_NOGP
@@ -255,8 +256,34 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int jlo = res_owner((long long)ctl[1] * W4, Q, a.g);
     const int jhi = res_owner((long long)(ctl[2] + 1) * W4 - 1, Q, a.g);
     const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
-    const float WWf = (float)WW;
-    const int lbase = RX - rlo * WW;
+    // Every tap's bilinear geometry is iteration-invariant, so it is resolved once:
+    // the fractional parts lh = h - floor(h), lw = w - floor(w) (.cuh:35-36, the same
+    // values the per-iteration form computes) and the window cell of the footprint's
+    // top-left corner as a float index into fwin/fwinB (the copy that makes the
+    // horizontal pair 8-byte aligned), two 16-bit indices per register.  An iteration
+    // then spends no VALU on floors or addresses.
+    float lhv[K][4], lwv[K][4];
+    unsigned adp[K][2];
+    {
+        const float WWf = (float)WW;
+        const int lbase = RX - rlo * WW, bofs = a.wh_max * WW - 1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            adp[k][0] = adp[k][1] = 0u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float fh = floorf(hy[k][e]), fw = floorf(hx[k][e]);
+                lhv[k][e] = hy[k][e] - fh;
+                lwv[k][e] = hx[k][e] - fw;
+                // window index (h_low - rlo) * WW + w_low + RX, in exact float arithmetic;
+                // out-of-window (general-path) taps are clamped to cell 0 and never read
+                int li = (int)(fh * WWf + fw) + lbase;
+                li = ((unsigned)li < (unsigned)(WH * WW)) ? li : 0;
+                const unsigned idx = (li & 1) ? (unsigned)(li + bofs) : (unsigned)li;
+                adp[k][e >> 1] |= idx << (16 * (e & 1));
+            }
+        }
+    }
 
     const T *p_all = static_cast<const T *>(a.pred_inter);
     T *p_out_all = static_cast<T *>(a.pred_inter);
@@ -267,9 +294,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // compiler would hoist all 32 taps' weights and addresses out of this loop
         // and spill them; opaque register moves keep them per iteration (no code).
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(hy[k][e]), "+v"(hx[k][e]));
+            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
+            asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
+        }
         int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
         asm volatile("" : "+v"(tb));
 
@@ -352,15 +381,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const float h_im = hy[k][e], w_im = hx[k][e];
-                    const float fh = floorf(h_im), fw = floorf(w_im);
-                    const float lh = h_im - fh, lw = w_im - fw;  // = h - (float)h_low (.cuh:35-36)
+                    const float lh = lhv[k][e], lw = lwv[k][e];  // = h - (float)h_low (.cuh:35-36)
                     const float hh = 1.f - lh, hw = 1.f - lw;
                     const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    // window index (h_low - rlo) * WW + w_low + RX, in exact float arithmetic
-                    const int li = (int)(fh * WWf + fw) + lbase;
-                    const int par = li & 1;
-                    const float2 *sp = reinterpret_cast<const float2 *>((par ? fwinB : fwin) + (li - par));
+                    const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
+                    const float2 *sp = reinterpret_cast<const float2 *>(fwin + idx);
                     const float2 s01 = sp[0], s23 = sp[WW / 2];
                     const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                     acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
