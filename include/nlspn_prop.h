@@ -130,9 +130,12 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
                     unsigned flags, void *stream);
 
 /*
- * Graph plans: nlspn_propagate captured once into a hipGraph (T kernel nodes)
- * and replayed with one hipGraphLaunch.  Pointers are baked in at creation;
- * γ stays live because it is read from device memory.
+ * Plans: nlspn_propagate captured once into a hipGraph (T kernel nodes) and
+ * replayed with one hipGraphLaunch.  Pointers are baked in at creation; γ stays
+ * live because it is read from device memory.  A plan of at most two launches
+ * (step 1 + the resident kernel) re-issues its recorded launches directly
+ * instead, which costs less than a graph launch; NLSPN_PLAN_GRAPH=1 forces the
+ * graph.
  */
 typedef struct nlspn_plan *nlspn_plan_t;
 int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep,

@@ -145,7 +145,19 @@ int prepare_step(StepReq &r, StepLaunch &L) {
                                       : select_step<__half>(a, r.kh, r.kw, a.off != nullptr, vec, r.first, L);
 }
 
+// A plan's launch record: enough to re-issue one kernel launch without a graph.
+struct LaunchRec {
+    const void *fn;
+    dim3 grid, block;
+    size_t lds;
+    bool resident;
+    StepArgs sa;
+    ResArgs ra;
+};
+thread_local std::vector<LaunchRec> *g_rec = nullptr;  // set while nlspn_plan_create records
+
 int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    if (g_rec) g_rec->push_back(LaunchRec{L.fn, L.grid, L.block, 0, false, a, ResArgs{}});
     void *args[] = {&a};
     if (e0)
         NLSPN_HIP_TRY(hipExtLaunchKernel(L.fn, L.grid, L.block, args, 0, s, e0, e1, 0));
@@ -241,6 +253,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
 // The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words).
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
+    if (g_rec) g_rec->push_back(LaunchRec{P.fn, dim3(P.grid), dim3(P.block), P.lds, true, StepArgs{}, P.a});
     void *args[] = {&P.a};
     if (e0)
         NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s, e0, e1, 0));
@@ -444,9 +457,18 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
                           as_stream(stream), nullptr, nullptr);
 }
 
+// A plan replays the captured section as one hipGraph, except when it is at most
+// kPlanDirectMax launches (the resident path: step 1 + one resident launch): there
+// a graph launch costs more than the launches it saves (C2: 152.5 vs 147.3 us per
+// step, tools/launch_probe.py), so the recorded launches are re-issued directly.
+// NLSPN_PLAN_GRAPH=1 forces the graph.
+constexpr size_t kPlanDirectMax = 2;
+
 struct nlspn_plan {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    std::vector<LaunchRec> recs;
+    bool direct = false;
 };
 
 int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -462,9 +484,12 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
         (void)hipStreamDestroy(cs);
         return fail(NLSPN_EHIP, "hipStreamBeginCapture: %s", hipGetErrorString(e));
     }
+    std::vector<LaunchRec> recs;
+    g_rec = &recs;
     int rc = nlspn_propagate(dtype, pred_init, dep, conf, aff_raw, aff_bstride, off_raw, off_bstride, gamma,
                              pred_inter, pred, aff_out, off_out, conf_out, workspace, B, H, W, kh, kw, T, kind,
                              flags, cs);
+    g_rec = nullptr;
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(cs, &g);
     (void)hipStreamDestroy(cs);
@@ -482,14 +507,24 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
     nlspn_plan *p = new nlspn_plan;
     p->graph = g;
     p->exec = ge;
+    const char *env = getenv("NLSPN_PLAN_GRAPH");
+    p->direct = recs.size() <= kPlanDirectMax && !(env && env[0] == '1');
+    p->recs = std::move(recs);
     *plan = p;
     return NLSPN_OK;
 }
 
 int nlspn_plan_launch(nlspn_plan_t plan, void *stream) {
     if (!plan) return fail(NLSPN_EINVAL, "plan is null");
-    NLSPN_HIP_TRY(hipGraphLaunch(plan->exec, as_stream(stream)));
-    return NLSPN_OK;
+    if (!plan->direct) {
+        NLSPN_HIP_TRY(hipGraphLaunch(plan->exec, as_stream(stream)));
+        return NLSPN_OK;
+    }
+    for (LaunchRec &r : plan->recs) {
+        void *args[] = {r.resident ? static_cast<void *>(&r.ra) : static_cast<void *>(&r.sa)};
+        NLSPN_HIP_TRY(hipLaunchKernel(r.fn, r.grid, r.block, args, r.lds, as_stream(stream)));
+    }
+    return check_launch("nlspn_plan_launch");
 }
 
 int nlspn_plan_destroy(nlspn_plan_t plan) {

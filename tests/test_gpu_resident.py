@@ -93,6 +93,34 @@ def test_resident_bitexact_vs_steps(B, H, W, sigma, dtype, conf, kw):
     assert torch.equal(a["pred"], b["pred"])
 
 
+@pytest.mark.parametrize("T", [2, 3, 36])
+def test_resident_bitexact_short_and_long(T):
+    inp, _ = _inputs(4, 64, 128, sigma=3.0)
+    a, b = _both(inp, T=T)
+    assert torch.equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
+    assert torch.equal(a["pred"], b["pred"])
+
+
+def test_plan_direct_equals_graph():
+    """The resident plan re-issues its two launches directly; forcing the hipGraph
+    replay gives the same bits."""
+    inp, _ = _inputs(8, 228, 304, sigma=2.0, seed=5)
+    outs = []
+    for graph in ("0", "1"):
+        os.environ["NLSPN_PLAN_GRAPH"] = graph
+        try:
+            with _env("1"):
+                plan = PropagationPlan(*inp, prop_time=18)
+                plan.replay()
+                plan.replay()
+                torch.cuda.synchronize()
+                outs.append(plan.outputs["pred_inter"].clone())
+                plan.close()
+        finally:
+            os.environ.pop("NLSPN_PLAN_GRAPH", None)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_resident_nonfinite_offsets():
     inp, _ = _inputs(2, 64, 128)
     off = inp[4].clone()

@@ -52,5 +52,5 @@ def run(B=8, H=228, W=304, T=18, reps=20, dbgs=(0, 1, 2, 4, 3, 6, 7), resident=(
 if __name__ == "__main__":
     args = dict(a.split("=") for a in sys.argv[1:])
     run(B=int(args.get("B", 8)), H=int(args.get("H", 228)), W=int(args.get("W", 304)), T=int(args.get("T", 18)),
-        resident=tuple(args.get("resident", "1,0").split(",")),
+        resident=tuple(args.get("resident", "1,0").split(",")), reps=int(args.get("reps", 20)),
         dbgs=tuple(int(x) for x in args.get("dbgs", "0,1,2,4,3,6,7").split(",")))
