@@ -230,12 +230,12 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
         }
         nt = (qmax + 63) / 64 * 64;
         if (nt > kResMaxNT) break;  // fewer parts only makes them larger
-        const long long avail = (long long)kLdsBytes - 16 - 16LL * 9 * nt;
+        const long long avail = (long long)kLdsBytes - 16 - 16LL * 10 * nt;
         wh_max = avail > 0 ? avail / (2 * WWb) : 0;  // two copies of the window
         if (wh_max >= rows_max + 2 * kResRY) break;
     }
     if (g < 1 || nt > kResMaxNT || wh_max < 1) return false;
-    const size_t lds = 16 + (size_t)(2 * wh_max * WWb) + 16 * 9 * (size_t)nt;
+    const size_t lds = 16 + (size_t)(2 * wh_max * WWb) + 16 * 10 * (size_t)nt;
     if (lds > kLdsBytes || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
     const unsigned G = (unsigned)(B * g);
     if ((G + 1) * 4 > kSyncBytes) return false;

@@ -81,6 +81,11 @@ __device__ __forceinline__ int res_owner(long long q, long long Q, int g) {
     return (int)(((q + 1) * g - 1) / Q);
 }
 
+// A value as storage type T holds it (fp32: itself; fp16: rounded), back in fp32.
+template <typename T> __device__ __forceinline__ float round_to(float v);
+template <> __device__ __forceinline__ float round_to<float>(float v) { return v; }
+template <> __device__ __forceinline__ float round_to<__half>(float v) { return (float)(_Float16)v; }
+
 template <typename T> struct ResVec;  // 4 contiguous elements <-> float[4], buffer access with cache bits
 template <> struct ResVec<float> {
     template <unsigned AUX>
@@ -128,7 +133,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (s[rx], s[rx+1]) is ONE 8-byte-aligned ds_read_b64 from one of the copies
     float *fwin = smem + 4;                                                      // [wh_max][WW]
     float *fwinB = fwin + (size_t)a.wh_max * WW;                                 // [wh_max][WW], shifted by 1
-    float4 *akl = reinterpret_cast<float4 *>(fwinB + (size_t)a.wh_max * WW);  // [K+1][NT]: affinities, 1 - sum
+    // [K+2][NT]: affinities, 1 - sum, and the own quad's conf' (1 with conf_prop off)
+    float4 *akl = reinterpret_cast<float4 *>(fwinB + (size_t)a.wh_max * WW);
     const int NT = blockDim.x;
     const int tid = threadIdx.x, lane = tid & 63;
 
@@ -178,6 +184,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) akl[k * NT + tid] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
         akl[K * NT + tid] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+        float cq[4] = {1.f, 1.f, 1.f, 1.f};
+        if (has_conf) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), vpix, 0u, cq);
+        akl[(K + 1) * NT + tid] = make_float4(cq[0], cq[1], cq[2], cq[3]);
     }
 
     // ---- the window: every row a valid tap of this part touches (offsets are
@@ -215,6 +224,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int WH = rhi - rlo + 1;
     const int ra = rlo < 0 ? 0 : rlo, rb = rhi > H - 1 ? H - 1 : rhi;  // in-image window rows
     const int nsq = (rb - ra + 1) * W4;                                // staging quads per iteration
+    const int iown0 = (int)(qlo - (long long)ra * W4), iown1 = (int)(qhi - (long long)ra * W4);  // own ones
     __syncthreads();
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
@@ -334,13 +344,16 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // (written by other parts in this launch), conf' by plain loads (invariant)
         const T *p_in = p_all + (size_t)(t - 1) * N + b * HW;
         const rsrc_t rp = make_rsrc(p_in);
-        const int nsq_it = (a.dbg & 2u) ? 0 : nsq;
+        // t >= 2: the own quads are in the window already (written back below), so
+        // only the other parts' quads are loaded
+        const int nown = t >= 2 ? iown1 - iown0 : 0;
+        const int nsq_it = (a.dbg & 2u) ? 0 : nsq - nown;
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                const int i = base + s * NT;
-                if (i < nsq_it) {
+                const int k = base + s * NT, i = k < iown0 ? k : k + nown;
+                if (k < nsq_it) {
                     const int r = ra + i / W4, c = (i % W4) * 4;
                     const unsigned go = (unsigned)(r * W + c) * ES;
                     ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
@@ -349,8 +362,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                const int i = base + s * NT;
-                if (i < nsq_it) {
+                const int k = base + s * NT, i = k < iown0 ? k : k + nown;
+                if (k < nsq_it) {
                     const int r = ra + i / W4, c = (i % W4) * 4;
                     float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
                     if (has_conf) {
@@ -367,6 +380,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         lds_barrier();
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
+        float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
         if (active && !(a.dbg & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             // branch-free path: every tap from the LDS window (invalid taps read zeros)
@@ -460,12 +474,28 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
             T *p_out = p_out_all + (size_t)t * N + b * HW;
             ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1) ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
         }
         // ---- publish: every wave drains its write-through stores, then ONE lane
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_store(&sync[blockIdx.x], (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
+        // this iteration is done: the barrier above), as the next staging would load it
+        if (t < a.T - 1 && active && !(a.dbg & 2u)) {
+            const float4 cw = akl[(K + 1) * NT + tid];
+            float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
+            if (has_conf) {
+                f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
+            }
+            const int li = (y - rlo) * WW + RX + x0;
+            *reinterpret_cast<float4 *>(&fwin[li]) = f;
+            fwinB[li - 1] = f.x;
+            *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
+            fwinB[li + 2] = f.w;
+        }
     }
 }
 
