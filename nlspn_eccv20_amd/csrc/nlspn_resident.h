@@ -62,7 +62,8 @@ struct ResArgs {
     int g;              // parts (workgroups) per image
     int wh_max;         // LDS window rows allocated per buffer
     unsigned flags;
-    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps
+    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
+                        // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid)
 };
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
@@ -312,6 +313,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
         asm volatile("" : "+v"(tb));
 
+        unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
+                                                      ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
+        if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
         // ---- wait until every part this one reads has finished iteration t-1
         if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
@@ -339,6 +343,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
         if (ctl[0]) return;
+        if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
 
         // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
         // (written by other parts in this launch), conf' by plain loads (invariant)
@@ -378,6 +383,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
         lds_barrier();
+        if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
@@ -476,11 +482,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);
 #pragma unroll
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
-            if (t == a.T - 1) ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
+            if (t == a.T - 1 && !(a.dbg & 8u))
+                ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
         }
         // ---- publish: every wave drains its write-through stores, then ONE lane
+        if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0) __hip_atomic_store(&sync[blockIdx.x], (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
         // this iteration is done: the barrier above), as the next staging would load it

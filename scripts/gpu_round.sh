@@ -17,6 +17,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_nyu -o nyu --output-format csv -- \
     python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-backward > $O/stats_nyu.log 2>&1 &&
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_$C -o run --output-format csv -- \
-      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-backward --kernel-reps 5 > $O/pmc_$C.log 2>&1 || exit 1
+  NLSPN_PLAN_GRAPH=1 timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_$C -o run --output-format csv -- \
+      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-backward --no-gru --kernel-reps 5 > $O/pmc_$C.log 2>&1 || exit 1
 done
