@@ -155,6 +155,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // ---- own quad and its invariants (registers for the whole launch).  Taps are
     // held as their sample coordinates (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw),
     // the reference's own expression (.cuh:178-179), so an iteration starts from them.
+    // trace (dbg 8): row t = 0 of this part holds the setup stamps
+    unsigned long long *trace0 = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
+                                                   (size_t)blockIdx.x * a.T * 5 : nullptr;
+    if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
     const long long q = qlo + tid;
     const bool active = q < qhi;
     const int y = active ? (int)(q / W4) : 0, x0 = active ? (int)(q % W4) * 4 : 0;
@@ -195,6 +199,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // the part's rows +- RY, and the rare taps outside it take the general path.
     if (tid == 0) { ctl[0] = 0; ctl[1] = prow0; ctl[2] = prow1; }  // own rows: the reference tap
     __syncthreads();
+    if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
     const float Hf = (float)H, Wf = (float)W;
     {
         int mn = prow0, mx = prow1;
@@ -230,6 +235,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     __syncthreads();
+    if (trace0 && tid == 0) trace0[2] = __builtin_amdgcn_s_memrealtime();
     // Classify every tap once:
     //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
     //    coordinates are redirected to (rlo, -RX), an integer point of the window's
@@ -264,6 +270,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (has_fb) { atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); }
     }
     __syncthreads();
+    if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
     const int jlo = res_owner((long long)ctl[1] * W4, Q, a.g);
     const int jhi = res_owner((long long)(ctl[2] + 1) * W4 - 1, Q, a.g);
     const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes

@@ -36,8 +36,13 @@ def main(B=8, H=228, W=304, T=18, reps=5):
     torch.cuda.synchronize()
     os.environ.pop("NLSPN_RES_DBG")
     st = outs["pred"].view(-1).view(torch.int64)[: G * T * 5].cpu().numpy().reshape(G, T, 5).astype(np.float64)
-    st = st[:, 1:, :] / 100.0  # us; iterations 2..T
-    st -= st[:, 0, 0].min()
+    st = st / 100.0  # us
+    st -= st[:, 0, 0].min()  # row t = 0: setup stamps (entry, invariants loaded, window zeroed, taps classified)
+    su = st[:, 0, :]
+    setup = {"entry_spread": su[:, 0].max() - su[:, 0].min(), "invariant_loads": np.median(su[:, 1] - su[:, 0]),
+             "window": np.median(su[:, 2] - su[:, 1]), "classify": np.median(su[:, 3] - su[:, 2]),
+             "geometry_to_loop": np.median(st[:, 1, 0] - su[:, 3]), "first_loop_top_max": st[:, 1, 0].max()}
+    st = st[:, 1:, :]  # iterations 2..T
     ph = {"wait": st[:, :, 1] - st[:, :, 0], "stage": st[:, :, 2] - st[:, :, 1], "taps+store": st[:, :, 3] - st[:, :, 2],
           "drain+barrier": st[:, :, 4] - st[:, :, 3]}
     ph["loop"] = st[:, 1:, 0] - st[:, :-1, 4]
@@ -54,6 +59,7 @@ def main(B=8, H=228, W=304, T=18, reps=5):
     span = st[:, -1, 4].max() - st[:, 0, 0].min()
     out["span_us"] = round(float(span), 2)
     out["per_iter_us"] = round(float(span) / st.shape[1], 3)
+    out["setup"] = {k: round(float(v), 3) for k, v in setup.items()}
     print(json.dumps(out))
 
 
