@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before our library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnlspn_hip.so")
+# NLSPN_LIB_PATH: another build of the same ABI (A/B timing of library versions)
+LIB_PATH = os.environ.get("NLSPN_LIB_PATH") or os.path.join(_HERE, "lib", "libnlspn_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nlspn_prop.h")
 
 DTYPE_F32, DTYPE_F16 = 0, 1
