@@ -291,7 +291,12 @@ def main():
                                 if resident else f"{kname} (one fused iteration)"),
                      "pixel_iterations_per_launch": npx * iters,
                      "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5)},
+                     "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5),
+                     # the HBM rate the kernel really drives (PMC bytes / its duration)
+                     "traffic_gbs": round(traffic / (kmean * 1e-3) / 1e9, 1) if traffic else None,
+                     "note": ("achieved credits SURVEY 8(d)'s per-iteration algorithmic bytes; this kernel reads "
+                              "the invariant planes once (see traffic), so frac > 1 measures on-chip reuse, "
+                              "not HBM bandwidth" if resident else None)},
         "gpu_event_ms_per_step": round(gpu_ms / a.steps, 4),
     }
     if cfg["dtype"] == "f32" and not a.no_backward:
