@@ -4,7 +4,8 @@
 One "step" = the whole propagation section of NLSPNModel.forward
 (src/model/nlspnmodel.py:323-381) over one synthetic batch: the prologue
 (affinity normalisation, offset insertion, confidence/input blend) plus T fused
-iterations, replayed as one native hipGraph (nlspn_plan_launch).  Inputs are
+iterations, replayed through a native plan (nlspn_plan_launch: step 1 + the
+resident kernel re-issued directly, or one hipGraph of the T step launches).  Inputs are
 resident in HBM before the timed region.  value = iterations/s summed over all
 ranks = N * T * steps / max-over-ranks wall time.
 
