@@ -63,6 +63,23 @@ int nlspn_abi_version(void);
 const char *nlspn_last_error(void);
 
 /*
+ * S2D sparse-depth encoder front, fused.  Replaces the pool
+ * pyramid and pool_convs of S2D.forward (src/model/nlspnmodel.py:437-455) and the
+ * torch.cat([dep_feat, dep], 1) that feeds S2D.conv (:459):
+ *   dep  : B x H x W (sparse depth, 0 = missing)
+ *   w1 b1: pool_convs[0] conv weight (8 x 6) and bias (8); w2 b2: pool_convs[1]
+ *          weight (16 x 8) and bias (16); device float32
+ *   out  : B x 17 x H x W: channels 0..15 = ReLU(w2 . ReLU(w1 . pyramid + b1) + b2),
+ *          channel 16 = dep
+ *   pyr  : B x 6 x H x W, the min pools 3/5/7/9 (zeros = missing, :441-447) and max
+ *          pools 11/13 (:449-452), or NULL (written for the weight gradients)
+ * float32 only.
+ */
+int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *b1,
+                      const float *w2, const float *b2, void *out, void *pyr,
+                      int B, int H, int W, void *stream);
+
+/*
  * Affinity normalisation + reference-tap insertion.
  * Replaces NLSPNModel._affinity_normalization (src/model/nlspnmodel.py:179-201)
  * followed by _aff_insert (:261-269).

@@ -32,6 +32,7 @@ SIGNATURES = {
     "nlspn_abi_version": (_i, []),
     "nlspn_last_error": (ctypes.c_char_p, []),
     "nlspn_affinity_normalize": (_i, [_i, _vp, _i64, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nlspn_s2d_pyramid": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp]),
     "nlspn_prop_step": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i, _vp, _vp, _i, _i, _i, _i, _i, _u, _vp]),
     "nlspn_workspace_bytes": (_sz, [_i, _i, _i, _i]),
     "nlspn_propagate": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

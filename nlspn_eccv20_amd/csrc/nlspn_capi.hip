@@ -18,6 +18,7 @@
 #include "nlspn_backward.h"
 #include "nlspn_step.h"
 #include "nlspn_resident.h"
+#include "nlspn_s2d.h"
 
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
@@ -407,6 +408,21 @@ extern "C" {
 int nlspn_abi_version(void) { return NLSPN_ABI_VERSION; }
 
 const char *nlspn_last_error(void) { return g_err.c_str(); }
+
+int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *b1, const float *w2,
+                      const float *b2, void *out, void *pyr, int B, int H, int W, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "S2D pyramid: float32 only (dtype %d)", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (!dep || !w1 || !b1 || !w2 || !b2 || !out) return fail(NLSPN_EINVAL, "null required pointer");
+    S2DArgs a{static_cast<const float *>(dep), w1, b1, w2, b2, static_cast<float *>(out), static_cast<float *>(pyr),
+              B, H, W, (W + kS2DTW - 1) / kS2DTW, (H + kS2DTH - 1) / kS2DTH};
+    const long long grid = (long long)B * a.tiles_x * a.tiles_y;
+    if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&s2d_pyramid_kernel), dim3((unsigned)grid), dim3(256),
+                                  args, 0, as_stream(stream)));
+    return check_launch("nlspn_s2d_pyramid");
+}
 
 int nlspn_affinity_normalize(int dtype, const void *aff_raw, int64_t aff_bstride, const float *gamma,
                              void *aff_out, int B, int K, int H, int W, int kind, void *stream) {

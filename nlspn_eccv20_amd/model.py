@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from .propagation import affinity_normalization, kernel_geometry, off_insert, prop_step, propagate
+from .s2d import s2d_front
 
 __all__ = ["NLSPNModel", "ConvGRU", "S2D", "conv_bn_relu", "convt_bn_relu", "get_resnet18", "get_resnet34", "get",
            "SectionGraph"]
@@ -160,7 +161,10 @@ class S2D(nn.Module):
         self.conv = conv_bn_relu(16 + 1, 32, kernel=3, stride=1, bn=False)
 
     def forward(self, dep):
-        pyr = []
+        if dep.is_cuda and dep.dtype == torch.float32:  # the fused HIP front (s2d.py)
+            c0, c1 = self.pool_convs[0][0], self.pool_convs[1][0]
+            return self.conv(s2d_front(dep, c0.weight, c0.bias, c1.weight, c1.bias))
+        pyr = []  # CPU tensors (host-side model tests): the reference's torch ops
         for pool in self.min_pools:
             z = -pool(torch.where(dep == 0, -999 * torch.ones_like(dep), -dep))
             pyr.append(torch.where(z == 999, torch.zeros_like(dep), z))

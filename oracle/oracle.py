@@ -214,3 +214,34 @@ def mdcn_backward(inp, weight, offset, mask, grad_output, stride=(1, 1), padding
     if rc != 0:
         raise MemoryError("oracle mdcn backward: allocation failed")
     return gi, goff, gm, gw, gb
+
+
+def s2d_front(dep, w1, b1, w2, b2):
+    """S2D pool pyramid + pool_convs + concat (src/model/nlspnmodel.py:437-459), numpy.
+
+    dep (B, 1, H, W) sparse depth; w1 (8, 6[, 1, 1]), b1 (8), w2 (16, 8[, 1, 1]), b2 (16).
+    Min pools s = 3, 5, 7, 9 (:441-447): -maxpool(where(dep == 0, -999, -dep)) with the
+    pools' implicit -inf padding, then 999 -> 0; restated as the min over in-image cells
+    of (dep != 0 ? dep : 999).  Max pools s = 11, 13 (:449-452).  pool_convs: two 1x1
+    conv + ReLU (:455), accumulated in float64 and rounded once.  Returns
+    (out (B, 17, H, W) = [pool_convs output, dep], pyramid (B, 6, H, W)), float32."""
+    from numpy.lib.stride_tricks import sliding_window_view as swv
+
+    d = np.asarray(dep, np.float32)[:, 0]
+    B, H, W = d.shape
+    pyr = np.empty((B, 6, H, W), np.float32)
+    masked = np.where(d == 0, np.float32(999), d)
+    for i, r in enumerate((1, 2, 3, 4)):
+        p = np.pad(masked, ((0, 0), (r, r), (r, r)), constant_values=np.inf)
+        m = swv(p, (2 * r + 1, 2 * r + 1), axis=(1, 2)).min(axis=(-1, -2))
+        pyr[:, i] = np.where(m == 999, np.float32(0), m)
+    for i, r in enumerate((5, 6)):
+        p = np.pad(d, ((0, 0), (r, r), (r, r)), constant_values=-np.inf)
+        pyr[:, 4 + i] = swv(p, (2 * r + 1, 2 * r + 1), axis=(1, 2)).max(axis=(-1, -2))
+    w1 = np.asarray(w1, np.float64).reshape(8, 6)
+    w2 = np.asarray(w2, np.float64).reshape(16, 8)
+    h1 = np.maximum(np.einsum("oc,bchw->bohw", w1, pyr.astype(np.float64)) +
+                    np.asarray(b1, np.float64).reshape(1, 8, 1, 1), 0).astype(np.float32)
+    h2 = np.maximum(np.einsum("oc,bchw->bohw", w2, h1.astype(np.float64)) +
+                    np.asarray(b2, np.float64).reshape(1, 16, 1, 1), 0).astype(np.float32)
+    return np.concatenate([h2, d[:, None]], 1), pyr
