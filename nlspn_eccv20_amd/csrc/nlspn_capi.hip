@@ -415,7 +415,8 @@ int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *
     if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
     if (!dep || !w1 || !b1 || !w2 || !b2 || !out) return fail(NLSPN_EINVAL, "null required pointer");
     S2DArgs a{static_cast<const float *>(dep), w1, b1, w2, b2, static_cast<float *>(out), static_cast<float *>(pyr),
-              B, H, W, (W + kS2DTW - 1) / kS2DTW, (H + kS2DTH - 1) / kS2DTH};
+              B, H, W, (W + kS2DTW - 1) / kS2DTW, (H + kS2DTH - 1) / kS2DTH, 0u};
+    if (const char *d = getenv("NLSPN_S2D_DBG")) a.dbg = (unsigned)atoi(d);
     const long long grid = (long long)B * a.tiles_x * a.tiles_y;
     if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
     void *args[] = {&a};

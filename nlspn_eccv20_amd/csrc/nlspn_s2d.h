@@ -13,9 +13,8 @@
 // The 1x1 convs sum their input channels in index order from the bias; MIOpen's
 // order is not specified, so parity with the torch module is to a tolerance.
 //
-// Work decomposition: a 16 x 64 tile per 256-thread workgroup; thread t takes column
-// t % 64 of rows t / 64 + 4e (e = 0..3), so every store instruction writes 64
-// consecutive pixels of a plane; the tile's dep window (halo 6) staged once in LDS.  HBM: 4 B read +
+// Work decomposition: a 16 x 64 tile per 256-thread workgroup; the tile's dep window
+// (halo 6) staged once in LDS, the pools done separably through LDS (below).  HBM: 4 B read +
 // 68 B written per pixel (72 B/px, byte-bound); the pool window re-reads hit LDS.
 #pragma once
 
@@ -33,14 +32,20 @@ struct S2DArgs {
     float *pyr;         // B x 6 x H x W (the pool pyramid, for the weight gradients), or null
     int B, H, W;
     int tiles_x, tiles_y;
+    unsigned dbg;       // experiments only (NLSPN_S2D_DBG): 1 no pass 2 math, 2 no pass 1, 4 no stores
 };
 
 constexpr int kS2DTH = 16, kS2DTW = 64, kS2DR = 6;
 
+// Separable pools: pass 1 reduces every window row horizontally (masked min for
+// r = 1..4, max for r = 5, 6, nested, so each cell reads its 12 neighbours once);
+// pass 2 reduces those columns vertically.  Min and max are exact whatever the
+// order, so this equals the direct (2r+1)^2 reduction bit for bit.
 __global__ void __launch_bounds__(256) s2d_pyramid_kernel(S2DArgs a) {
     constexpr int TH = kS2DTH, TW = kS2DTW, R = kS2DR, WH = TH + 2 * R, WW = TW + 2 * R;
-    constexpr float NEG = -3.402823466e38f;  // "no cell": loses every max
+    constexpr float INF = __builtin_huge_valf();
     __shared__ float win[WH * WW];
+    __shared__ float hred[6][WH * TW];  // [r-1][row][col]: r <= 4 masked min, r = 5, 6 max
     __shared__ float wts[8 * 6 + 8 + 16 * 8 + 16];
     const int H = a.H, W = a.W;
     int tile = blockIdx.x;
@@ -66,53 +71,118 @@ __global__ void __launch_bounds__(256) s2d_pyramid_kernel(S2DArgs a) {
     }
     __syncthreads();
 
-    const int lx = threadIdx.x % TW, x = x0 + lx;
-    if (x >= W) return;  // no barrier below
-    const float *w1 = wts, *b1 = wts + 48, *w2 = wts + 56, *b2 = wts + 184;
-#pragma unroll 1
-    for (int e = 0; e < TH / 4; ++e) {
-        const int ly = threadIdx.x / TW + 4 * e, y = y0 + ly;
-        if (y >= H) break;
-        // ring by ring: the running min (masked) for r <= 4, the running max for r <= 6
-        float mn = 999.0f, mx = NEG, pyr[6];
+    // ---- pass 1: horizontal, every window row x tile column.  Out-of-image cells
+    // are the pools' -inf padding: skipped (a row outside the image: +inf / -inf).
+    for (int i = threadIdx.x; i < ((a.dbg & 2u) ? 0 : WH * TW); i += 256) {
+        const int r = i / TW, c = i % TW, gy = y0 - R + r, x = x0 + c;
+        float mn = INF, mx = -INF;
+        if (gy >= 0 && gy < H && x < W) {
+            const float *row = &win[r * WW + c + R];
+            const float v0 = row[0];
+            mn = v0 != 0.0f ? v0 : 999.0f;
+            mx = v0;
 #pragma unroll
-        for (int r = 0; r <= R; ++r) {
-            for (int dy = -r; dy <= r; ++dy) {
-                if (y + dy < 0 || y + dy >= H) continue;  // the pools' -inf padding
-                const int step = (dy == -r || dy == r) ? 1 : 2 * r;  // full edge rows, else the two side cells
-                for (int dx = -r; dx <= r; dx += step) {
-                    if (x + dx < 0 || x + dx >= W) continue;
-                    const float v = win[(ly + R + dy) * WW + lx + R + dx];
-                    if (r <= 4) mn = fminf(mn, v != 0.0f ? v : 999.0f);
+            for (int d = 1; d <= R; ++d) {
+                if (x - d >= 0) {
+                    const float v = row[-d];
+                    if (d <= 4) mn = fminf(mn, v != 0.0f ? v : 999.0f);
                     mx = fmaxf(mx, v);
                 }
+                if (x + d < W) {
+                    const float v = row[d];
+                    if (d <= 4) mn = fminf(mn, v != 0.0f ? v : 999.0f);
+                    mx = fmaxf(mx, v);
+                }
+                if (d <= 4) hred[d - 1][i] = mn;
+                else hred[d - 1][i] = mx;
             }
-            if (r >= 1 && r <= 4) pyr[r - 1] = mn == 999.0f ? 0.0f : mn;
-            if (r >= 5) pyr[r - 1] = mx;
+        } else {
+#pragma unroll
+            for (int d = 1; d <= R; ++d) hred[d - 1][i] = d <= 4 ? INF : -INF;
         }
-        // pool_convs (:455): two 1x1 conv + bias + ReLU, input channels in index order
-        float h1[8];
+    }
+    __syncthreads();
+
+    // ---- pass 2: vertical, then pool_convs.  Thread t takes the 4 pixels
+    // 4 (t % 16) .. +3 of row t / 16: the weights are read once per 4 pixels, and each
+    // output plane is one 16-byte store per lane (W % 4 == 0) or four dword stores.
+    const int ly = threadIdx.x / (TW / 4), lx = (threadIdx.x % (TW / 4)) * 4;
+    const int y = y0 + ly, x = x0 + lx;
+    if (y >= H || x >= W) return;  // no barrier below
+    const bool vec = (W & 3) == 0;
+    float pyr[4][6];
 #pragma unroll
-        for (int o = 0; o < 8; ++o) {
-            float s = b1[o];
+    for (int p = 0; p < 4; ++p) {
 #pragma unroll
-            for (int c = 0; c < 6; ++c) s += w1[o * 6 + c] * pyr[c];
-            h1[o] = fmaxf(s, 0.0f);
+        for (int r = 1; r <= R; ++r) {
+            const float *col = &hred[r - 1][(ly + R) * TW + lx + p];
+            float m = col[0];
+#pragma unroll
+            for (int d = 1; d <= r; ++d) {
+                m = r <= 4 ? fminf(m, col[-d * TW]) : fmaxf(m, col[-d * TW]);
+                m = r <= 4 ? fminf(m, col[d * TW]) : fmaxf(m, col[d * TW]);
+            }
+            pyr[p][r - 1] = (a.dbg & 1u) ? 0.f : (r <= 4 ? (m == 999.0f ? 0.0f : m) : m);
         }
-        const long long px = (long long)y * W + x;
-        float *out = a.out + (long long)b * 17 * HW + px;
+    }
+    // pool_convs (:455): two 1x1 conv + bias + ReLU, input channels in index order
+    float h1[4][8];
 #pragma unroll
-        for (int o = 0; o < 16; ++o) {
-            float s = b2[o];
+    for (int o = 0; o < 8; ++o) {
+        const float bo = wts[48 + o];
+        float wo[6];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) s += w2[o * 8 + c] * h1[c];
-            out[o * HW] = fmaxf(s, 0.0f);
+        for (int c = 0; c < 6; ++c) wo[c] = wts[o * 6 + c];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            float s = bo;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) s += wo[c] * pyr[p][c];
+            h1[p][o] = fmaxf(s, 0.0f);
         }
-        out[16 * HW] = win[(ly + R) * WW + lx + R];  // :459 torch.cat([dep_feat, dep], 1)
-        if (a.pyr) {
-            float *pp = a.pyr + (long long)b * 6 * HW + px;
+    }
+    const long long px = (long long)y * W + x;
+    float *out = a.out + (long long)b * 17 * HW + px;
+    auto put = [&](float *dst, const float (&v)[4]) {
+        if (a.dbg & 4u) {
+            if (v[0] == 12345.f) a.out[0] = v[1];  // keep the math alive
+            return;
+        }
+        if (vec) {
+            *reinterpret_cast<float4 *>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
 #pragma unroll
-            for (int c = 0; c < 6; ++c) pp[c * HW] = pyr[c];
+            for (int p = 0; p < 4; ++p)
+                if (x + p < W) dst[p] = v[p];
+        }
+    };
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+        const float bo = wts[184 + o];
+        float wo[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) wo[c] = wts[56 + o * 8 + c];
+        float v[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            float s = bo;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) s += wo[c] * h1[p][c];
+            v[p] = fmaxf(s, 0.0f);
+        }
+        put(out + o * HW, v);
+    }
+    {
+        const float *dw = &win[(ly + R) * WW + lx + R];
+        const float v[4] = {dw[0], dw[1], dw[2], dw[3]};
+        put(out + 16 * HW, v);  // :459 torch.cat([dep_feat, dep], 1)
+    }
+    if (a.pyr) {
+        float *pp = a.pyr + (long long)b * 6 * HW + px;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const float v[4] = {pyr[0][c], pyr[1][c], pyr[2][c], pyr[3][c]};
+            put(pp + c * HW, v);
         }
     }
 }
