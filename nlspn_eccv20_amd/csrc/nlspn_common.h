@@ -90,6 +90,8 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void *base) {
 // the load is narrowed to a single dword while the other lanes of the vector are
 // still read (garbage).  Bit-cast the WHOLE vector to a float/half vector first;
 // that form emits buffer_load_dwordx2/x4 correctly.
+constexpr unsigned kNT = 2u;  // buffer-instruction cache policy: nt (streaming, non-temporal)
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -103,8 +105,9 @@ template <> struct BVec<float, 1> {
     static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[1]) {
         v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[1]) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), r, vo, so, AUX);
     }
 };
 template <> struct BVec<float, 2> {
@@ -112,9 +115,10 @@ template <> struct BVec<float, 2> {
         const f32x2 q = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
         v[0] = q[0]; v[1] = q[1];
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[2]) {
         const f32x2 q = {v[0], v[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, AUX);
     }
 };
 template <> struct BVec<float, 4> {
@@ -122,17 +126,19 @@ template <> struct BVec<float, 4> {
         const f32x4 q = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
         v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
         const f32x4 q = {v[0], v[1], v[2], v[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q), r, vo, so, AUX);
     }
 };
 template <> struct BVec<__half, 1> {
     static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[1]) {
         v[0] = (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0));
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[1]) {
-        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v[0]), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v[0]), r, vo, so, AUX);
     }
 };
 template <> struct BVec<__half, 2> {
@@ -140,9 +146,10 @@ template <> struct BVec<__half, 2> {
         const f16x2 q = __builtin_bit_cast(f16x2, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
         v[0] = (float)q[0]; v[1] = (float)q[1];
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[2]) {
         const f16x2 q = {(_Float16)v[0], (_Float16)v[1]};
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, q), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, q), r, vo, so, AUX);
     }
 };
 template <> struct BVec<__half, 4> {
@@ -150,9 +157,10 @@ template <> struct BVec<__half, 4> {
         const f16x4 q = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
         v[0] = (float)q[0]; v[1] = (float)q[1]; v[2] = (float)q[2]; v[3] = (float)q[3];
     }
+    template <unsigned AUX = 0>
     static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[4]) {
         const f16x4 q = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, AUX);
     }
 };
 

@@ -242,8 +242,10 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
 #pragma unroll
             for (int c = 0; c < K + 1; ++c) {
                 const int k = c < REF ? c : c - 1;
-                BVec<T, PX>::store(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : dh[PRE ? k : 0]);
-                BVec<T, PX>::store(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : dw[PRE ? k : 0]);
+                // streaming (nt): the inserted offsets are an output only, never re-read here
+                BVec<T, PX>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : dh[PRE ? k : 0]);
+                BVec<T, PX>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes,
+                                                 c == REF ? z : dw[PRE ? k : 0]);
             }
         }
     }
