@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define NLSPN_ABI_VERSION 1
+#define NLSPN_ABI_VERSION 2
 
 /* element type of every tensor argument (math is always fp32) */
 #define NLSPN_DTYPE_F32 0
@@ -174,6 +174,9 @@ int nlspn_plan_destroy(nlspn_plan_t plan);
  * be NULL).  Writes grad_pred_init (B planes), grad_conf (B planes, iff conf),
  * grad_aff_raw (B x K planes, contiguous), grad_off_raw (B x 2K planes,
  * contiguous, iff off_raw), grad_gamma (1 float, TGASS only; may be NULL).
+ * grad_aff_bstride / grad_off_bstride: batch strides of grad_aff_raw / grad_off_raw
+ * in elements (0 = contiguous), so both can land in ONE packed (B, 3K, H, W)
+ * gradient of the head output the two slices came from (nlspnmodel.py:304-305).
  * dep receives no gradient (the reference's sparse input).  workspace:
  * nlspn_backward_workspace_bytes() bytes.  dL/df is scattered with float
  * atomics (as the reference's col2im), so its last bits depend on arrival order.
@@ -185,7 +188,8 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
                              const void *pred_inter, const void *aff_norm, const void *conf_eff,
                              const void *grad_pred, const void *grad_pred_inter,
                              void *grad_pred_init, void *grad_conf, void *grad_aff_raw,
-                             void *grad_off_raw, float *grad_gamma, void *workspace,
+                             int64_t grad_aff_bstride, void *grad_off_raw,
+                             int64_t grad_off_bstride, float *grad_gamma, void *workspace,
                              int B, int H, int W, int kh, int kw, int T, int kind,
                              unsigned flags, void *stream);
 

@@ -49,7 +49,7 @@ SIGNATURES = {
                                   _vp, _fp, _fp]),
     "nlspn_backward_workspace_bytes": (_sz, [_i, _i, _i, _i, _i]),
     "nlspn_propagate_backward": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                      _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _u, _vp]),
+                                      _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _u, _vp]),
     "nlspn_prop_step_backward_workspace_bytes": (_sz, [_i, _i, _i]),
     "nlspn_prop_step_backward": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _i, _i, _i, _i, _i, _u, _vp]),

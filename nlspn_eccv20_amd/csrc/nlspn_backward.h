@@ -55,7 +55,8 @@ struct BwdArgs {
     const float *aff_raw;   // raw head affinity, K planes per item at aff_raw_bs
     long long aff_raw_bs;
     const float *gamma;
-    float *grad_aff_raw;    // K planes per item, contiguous
+    float *grad_aff_raw;    // K planes per item, batch stride gaff_bs (0: K*H*W)
+    long long gaff_bs, goff_bs;  // batch strides of grad_aff_raw / g_off in elements (0: contiguous)
     float *gamma_part;      // one partial dL/dgamma per workgroup (TGASS), or null
     int kind;
 };
@@ -228,7 +229,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     const bool gins = a.g_aff_ins != 0;
     const rsrc_t rga = make_rsrc(a.g_aff + b * (gins ? K + 1 : K) * HW);
     auto gplane = [&](int k) { return (unsigned)(gins && k >= REF ? k + 1 : k) * plane_bytes; };
-    const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * 2 * K * HW : a.g_aff);
+    const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * (a.goff_bs ? a.goff_bs : 2LL * K * HW) : a.g_aff);
     float cG[K], cO[KO];
 #pragma unroll
     for (int k = 0; k < K; ++k) cG[k] = (HOIST && !last && !(DIAG & 4)) ? bld(rga, vpix, gplane(k)) : 0.f;
@@ -428,7 +429,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) ar[k] = bld(rar, vpix, (unsigned)k * plane_bytes);
             gsum = aff_norm_backward<K>(cG, ar, *a.gamma, a.kind, ga);
-            const rsrc_t rout = make_rsrc(a.grad_aff_raw + b * K * HW);
+            const rsrc_t rout = make_rsrc(a.grad_aff_raw + b * (a.gaff_bs ? a.gaff_bs : (long long)K * HW));
 #pragma unroll
             for (int k = 0; k < K; ++k) bst(rout, vpix, (unsigned)k * plane_bytes, ga[k]);
         } else if (!(DIAG & 4)) {

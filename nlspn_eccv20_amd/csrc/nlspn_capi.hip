@@ -668,9 +668,9 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
                              const void *aff_raw, int64_t aff_bstride, const void *off_raw, int64_t off_bstride,
                              const float *gamma, const void *pred_inter, const void *aff_norm, const void *conf_eff,
                              const void *grad_pred, const void *grad_pred_inter, void *grad_pred_init,
-                             void *grad_conf, void *grad_aff_raw, void *grad_off_raw, float *grad_gamma,
-                             void *workspace, int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags,
-                             void *stream) {
+                             void *grad_conf, void *grad_aff_raw, int64_t grad_aff_bstride, void *grad_off_raw,
+                             int64_t grad_off_bstride, float *grad_gamma, void *workspace, int B, int H, int W,
+                             int kh, int kw, int T, int kind, unsigned flags, void *stream) {
     if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the backward is implemented for float32 storage");
     if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
     if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
@@ -687,6 +687,11 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     if (aff_bstride < (long long)K * HW) return fail(NLSPN_EINVAL, "aff batch stride < K*H*W");
     if (off_raw && off_bstride < 2LL * K * HW) return fail(NLSPN_EINVAL, "offset batch stride < 2K*H*W");
     if (HW * (3LL * K + 4) * 4 > 0x7fffffffLL) return fail(NLSPN_EINVAL, "image too large for one batch item");
+    if (grad_aff_bstride < 0 || grad_off_bstride < 0 || (grad_aff_bstride && grad_aff_bstride < (long long)K * HW) ||
+        (grad_off_bstride && grad_off_bstride < 2LL * K * HW))
+        return fail(NLSPN_EINVAL, "gradient batch strides below K*H*W / 2K*H*W (0 = contiguous)");
+    if (grad_aff_bstride % 4 != 0 || grad_off_bstride % 4 != 0)
+        return fail(NLSPN_EINVAL, "gradient batch strides must be multiples of 4 elements");
     hipStream_t s = as_stream(stream);
     float *ws = static_cast<float *>(workspace);
     float *gf[2] = {ws, ws + N};
@@ -721,6 +726,8 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         a.gf_write = gf[(t - 1) & 1];
         a.g_aff = g_aff;
         a.g_off = static_cast<float *>(grad_off_raw);
+        a.goff_bs = grad_off_bstride;
+        a.gaff_bs = grad_aff_bstride;
         a.g_conf = conf ? g_conf : nullptr;
         a.off_bs = off_bstride;
         a.B = B; a.H = H; a.W = W;

@@ -301,7 +301,10 @@ class _PropagateFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pred_init, dep, confidence, aff, offset, gamma, prop_time, affinity, kernel, preserve_input,
-                always_clip, return_offset):
+                always_clip, return_offset, packed=None):
+        # packed: the (B, 3K, H, W) head output `offset` and `aff` are slices of
+        # (nlspnmodel.py:304-305); its gradient is then built in one buffer
+        ctx.packed = packed is not None
         kh, kw = kernel_geometry(kernel)
         outs = _alloc_outputs(pred_init, kh * kw - 1, prop_time, offset is not None and return_offset,
                               confidence is not None)
@@ -331,8 +334,13 @@ class _PropagateFn(torch.autograd.Function):
         g_inter = None if g_inter is None else g_inter.contiguous()
         g_pi = torch.empty((B, 1, H, W), **f32)
         g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
-        g_aff = torch.empty((B, K, H, W), **f32)
-        g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+        if ctx.packed:  # one (B, 3K, H, W) gradient: offsets in planes 0..2K-1, affinity after
+            g_oa = torch.empty((B, 3 * K, H, W), **f32)
+            g_off, g_aff, gbs = g_oa[:, :2 * K], g_oa[:, 2 * K:], 3 * K * H * W
+        else:
+            g_aff = torch.empty((B, K, H, W), **f32)
+            g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+            gbs = 0
         g_gamma = torch.zeros(1, **f32)
         lib = _lib.get()
         ws = torch.empty(lib.nlspn_backward_workspace_bytes(B, H, W, kh, kw) // 4, **f32)
@@ -344,10 +352,31 @@ class _PropagateFn(torch.autograd.Function):
             _lib.check(lib.nlspn_propagate_backward(
                 _lib.DTYPE_F32, _ptr(pred_init), _ptr(dep), _ptr(conf), _ptr(aff), abs_, _ptr(off), obs, _ptr(g),
                 _ptr(pred_inter), _ptr(aff_norm), _ptr(conf_eff), _ptr(g_pred), _ptr(g_inter), _ptr(g_pi),
-                _ptr(g_conf), _ptr(g_aff), _ptr(g_off), _ptr(g_gamma), _ptr(ws), B, H, W, kh, kw, T,
+                _ptr(g_conf), _ptr(g_aff), gbs, _ptr(g_off), gbs, _ptr(g_gamma), _ptr(ws), B, H, W, kh, kw, T,
                 _lib.AFF_KINDS[affinity], flags, _stream(dev)))
         g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype) if affinity == "TGASS" else None
-        return (g_pi, None, g_conf, g_aff, g_off, g_gamma) + (None,) * 6
+        if ctx.packed:
+            return (g_pi, None, g_conf, None, None, g_gamma) + (None,) * 6 + (g_oa,)
+        return (g_pi, None, g_conf, g_aff, g_off, g_gamma) + (None,) * 7
+
+
+def _packed_head(aff, offset):
+    """The contiguous (B, 3K, H, W) tensor that `offset` (planes 0..2K-1) and `aff`
+    (planes 2K..3K-1) are slices of, when it requires grad (nlspnmodel.py:304-305 slice
+    the head output so): autograd then gets ONE gradient for it instead of two
+    zero-filled full-size ones summed.  None otherwise."""
+    if offset is None or aff._base is None or offset._base is not aff._base:
+        return None
+    base = aff._base
+    if not base.requires_grad or base.dim() != 4 or not base.is_contiguous() or base.dtype != torch.float32:
+        return None
+    B, K = aff.shape[0], aff.shape[1]
+    HW = aff.shape[2] * aff.shape[3]
+    es = base.element_size()
+    if (tuple(base.shape) != (B, 3 * K, aff.shape[2], aff.shape[3]) or offset.data_ptr() != base.data_ptr()
+            or aff.data_ptr() != base.data_ptr() + 2 * K * HW * es or offset.shape[1] != 2 * K):
+        return None
+    return base
 
 
 def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: Optional[torch.Tensor],
@@ -363,9 +392,10 @@ def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: 
     (inserted, or None), 'aff' (normalised, K+1 taps), 'confidence' (blended, or None)}.
     Differentiable in pred_init, confidence, aff, offset and gamma when autograd is on.
     """
+    packed = _packed_head(aff, offset) if torch.is_grad_enabled() else None
     pred, pred_inter, aff_o, off_o, conf_o = _PropagateFn.apply(
         pred_init, dep, confidence, aff, offset, gamma, prop_time, affinity, kernel, preserve_input, always_clip,
-        return_offset)
+        return_offset, packed)
     return {"pred": pred, "pred_inter": list(pred_inter.unbind(0)), "offset": off_o, "aff": aff_o,
             "confidence": conf_o, "pred_inter_tensor": pred_inter}
 

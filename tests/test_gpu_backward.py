@@ -102,3 +102,25 @@ def test_module_trains(oracle):
     out["pred"].mean().backward()
     assert all(x.grad is not None and torch.isfinite(x.grad).all() for x in (pi, cf, oa))
     assert m.aff_scale_const.grad is not None and m.w.grad is None
+
+
+def test_packed_head_gradient_equals_separate_slices():
+    """offset/aff sliced from one (B, 3K, H, W) head output get ONE packed gradient
+    (propagation._packed_head); it equals the gradients of separate leaf tensors."""
+    K, B, H, W, T = 8, 2, 48, 64, 6
+    s = synth(B, H, W, K, seed=4, density=0.05, off_sigma=2.0)
+    t = lambda x, rg=True: torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(rg)  # noqa: E731
+    gp = torch.randn((B, 1, H, W), device=DEV)
+    grads = []
+    for packed in (True, False):
+        oa = t(s["off_aff"])
+        if packed:
+            off, aff = oa[:, :2 * K], oa[:, 2 * K:]
+        else:
+            off, aff = t(s["off_aff"][:, :2 * K]), t(s["off_aff"][:, 2 * K:])
+        g = torch.tensor([4.0], device=DEV, requires_grad=True)
+        o = propagate(t(s["pred_init"]), t(s["dep"], False), t(s["conf"]), aff, off, g, prop_time=T)
+        torch.autograd.backward(o["pred"], gp)
+        torch.cuda.synchronize()
+        grads.append(oa.grad if packed else torch.cat([off.grad, aff.grad], 1))
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-5, atol=1e-6)
