@@ -44,3 +44,4 @@ def test_oracle_matches_reference_ops():
 
 def test_library_exports_s2d():
     assert hasattr(_lib.get(), "nlspn_s2d_pyramid")
+
