@@ -5,30 +5,43 @@ One "step" = the whole propagation section of NLSPNModel.forward
 (src/model/nlspnmodel.py:323-381) over one synthetic batch: the prologue
 (affinity normalisation, offset insertion, confidence/input blend) plus T fused
 iterations, replayed through a native plan (nlspn_plan_launch: step 1 + the
-resident kernel re-issued directly, or one hipGraph of the T step launches).  Inputs are
+resident kernel re-issued directly, or the T step launches).  Inputs are
 resident in HBM before the timed region.  value = iterations/s summed over all
 ranks = N * T * steps / max-over-ranks wall time.
 
-Default workload = BASELINE config C2 (configs[1]): NYUv2 228x304, K=8, T=18,
-B=8, fp32, learned offsets (DCN path), TGASS.  --config kitti = C3, nyu_k16 = C5.
-Multi-GPU (torchrun): every rank runs its own batch (weak scaling, no collective
-on the data path) — the all_reduce below only takes the max time.
+Workloads (BASELINE.json configs):
+  headline (--config, default nyu) = C2: NYUv2 228x304, K=8, T=18, B=8, fp32,
+      learned offsets (DCN path), TGASS — the configuration `value` is quoted on;
+  "configs" object (same timing, roofline and PMC fields, per rank):
+      C3 kitti    KITTI-DC 240x1216, K=8, T=18, B=4 fp32 (at N=8: C4, B=32 global),
+      C5 nyu_k16  NYUv2, K=16 (1x17), T=36, B=16, fp16 storage,
+      C1 nyu_b1   NYUv2 B=1 (the CPU config's workload, on the GPU).
 
-Extra JSON objects:
-  roofline     — the dominant kernel: the resident kernel (iterations 2..T in
-                 one launch) where it applies, else the per-iteration step kernel.
-                 achieved = algorithmic bytes per launch (S*(4+3K) per
-                 pixel-iteration, SURVEY §8(d), x the pixel-iterations one launch
-                 processes) / its mean duration from dispatch-recorded HIP events
-                 (nlspn_time_propagate) on this stream; traffic = HBM bytes per
-                 launch from profiles/pmc_<config>.json (rocprofv3 PMC) when present.
-  backward     — (fp32 configs) forward+backward of the section through autograd
-                 (nlspn_propagate + nlspn_propagate_backward), ms per step and per
-                 iteration, HIP-event timed on this stream; not part of `value`.
-  gru_section  — (fp32, 3x3) the GRU-mode section (the reference's default), eager
-                 vs one hipGraph (SectionGraph); not part of `value`.
-  cpu_baseline — the C oracle (kind "port"; the reference has no CPU DCN path)
-                 on the same workload, rank 0, N=1.
+Multi-GPU: `--gpus N` without a torchrun environment spawns N ranks itself
+(nlspn_eccv20_amd.launch.spawn_local; the parent never touches the GPU).  Each rank
+runs its own batch shard (weak scaling, no collective on the data path; SURVEY
+§8e); the process group only carries the max-over-ranks timing and the per-rank
+spread.  `--dry-run` runs the launcher and sharding logic on CPU (gloo, no GPU).
+
+roofline (the dominant kernel: the resident kernel, iterations 2..T in one launch,
+where it applies, else the per-iteration step kernel):
+  achieved = COMPULSORY bytes per launch / its mean duration from dispatch-recorded
+      HIP events (nlspn_time_propagate) on this stream.  Compulsory bytes are what
+      the launch must move at least once: a step launch reads its 3K+3 input
+      planes and writes one (SURVEY §8(d)'s S*(4+3K) per pixel); the resident launch
+      reads the 3K+2 invariant planes and p_1 once and writes T-1 planes + pred.
+      So frac <= 1 for any kernel that really moves its bytes.
+  alg_8d   = the secondary figure on SURVEY §8(d)'s per-iteration basis
+      (S*(4+3K) bytes per pixel-iteration x the pixel-iterations of one launch),
+      which credits the resident kernel with re-reads it does not do (can exceed 1).
+  section  = the whole section's compulsory bytes (3K+3 planes read, T+3K+5
+      written) / ms_per_step.
+  traffic  = HBM-side bytes per launch from profiles/pmc_<config>.json (rocprofv3
+      FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes), or null.
+Extra objects (headline config only, not part of `value`): backward (fp32
+forward+backward through autograd), gru_section (the reference's default GRU mode),
+cpu_baseline (rank 0, N=1; the C oracle for the offset path and the reference's
+own torch op sequence for the no-offset path, all threads and 1 thread).
 """
 from __future__ import annotations
 
@@ -40,15 +53,14 @@ import statistics
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from nlspn_eccv20_amd import _lib  # noqa: E402
-from nlspn_eccv20_amd.propagation import PropagationPlan, _ptr, _stream, propagate  # noqa: E402
-from nlspn_eccv20_amd.sharding import max_over_ranks  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from nlspn_eccv20_amd import launch  # noqa: E402
+from nlspn_eccv20_amd.sharding import gather_over_ranks, max_over_ranks, shard_range  # noqa: E402
 from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
 
 CONFIGS = {
@@ -58,7 +70,11 @@ CONFIGS = {
                   B=4, H=240, W=1216, kernel=(3, 3), T=18, dtype="f32", max_depth=90.0, density=0.05),
     "nyu_k16": dict(id="C5", desc="NYUv2 228x304, K=16 (1x17), T=36, B=16, fp16 storage, learned offsets, TGASS",
                     B=16, H=228, W=304, kernel=(1, 17), T=36, dtype="f16", max_depth=10.0, density=500 / (228 * 304)),
+    "nyu_b1": dict(id="C1", desc="NYUv2 228x304, K=8, T=18, B=1, fp32, learned offsets, TGASS (C1's workload on "
+                                 "the GPU)",
+                   B=1, H=228, W=304, kernel=(3, 3), T=18, dtype="f32", max_depth=10.0, density=500 / (228 * 304)),
 }
+EXTRA = ("kitti", "nyu_k16", "nyu_b1")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -70,7 +86,7 @@ def baseline_metric():
         return "propagation iters/sec (+ ms/iter)"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -78,19 +94,34 @@ def parse():
     ap.add_argument("--config", default="nyu", choices=sorted(CONFIGS))
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-backward", action="store_true")
     ap.add_argument("--no-gru", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true")
     ap.add_argument("--backward-steps", type=int, default=20)
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="launcher + sharding only, on CPU (gloo)")
+    return ap.parse_args(argv)
+
+
+def make_inputs(cfg, rank, dev):
+    """Seeded synthetic head outputs of this rank's shard, in HBM."""
+    tdt = torch.float16 if cfg["dtype"] == "f16" else torch.float32
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    s = synth(cfg["B"], cfg["H"], cfg["W"], K, seed=7240 + rank, density=cfg["density"], max_depth=cfg["max_depth"])
+    to = lambda x: torch.from_numpy(x).to(dev, tdt)  # noqa: E731
+    off_aff = to(s["off_aff"])
+    inputs = {"pred_init": to(s["pred_init"]), "dep": to(s["dep"]), "conf": to(s["conf"]),
+              "aff": off_aff[:, 2 * K:], "off": off_aff[:, :2 * K], "gamma": torch.tensor([0.5 * K], device=dev)}
+    return inputs, s
 
 
 def kernel_time(plan, inputs, cfg, reps, dev):
     """Dispatch-recorded HIP-event durations (nlspn_time_propagate) on this stream, over
     `reps` whole propagations on the plan's buffers: step 1 (prologue fused) and
     iterations 2..T — one resident-kernel launch, or the sum of the T-1 step kernels."""
+    from nlspn_eccv20_amd import _lib
+    from nlspn_eccv20_amd.propagation import _ptr, _stream
     o = plan.outputs
-    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
     aff, off = inputs["aff"], inputs["off"]
     first, rest, res = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
     dt = _lib.DTYPE_F16 if cfg["dtype"] == "f16" else _lib.DTYPE_F32
@@ -100,7 +131,6 @@ def kernel_time(plan, inputs, cfg, reps, dev):
         _ptr(o["offset"]), _ptr(o["confidence"]), _ptr(o["workspace"]), cfg["B"], cfg["H"], cfg["W"],
         cfg["kernel"][0], cfg["kernel"][1], cfg["T"], _lib.AFF_KINDS["TGASS"], _lib.PRESERVE_INPUT, reps,
         _stream(dev), ctypes.byref(first), ctypes.byref(rest), ctypes.byref(res)))
-    assert K == aff.shape[1]
     return first.value, rest.value, bool(res.value)
 
 
@@ -119,9 +149,97 @@ def pmc_traffic(config, kernel):
     return None
 
 
+def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
+    """Roofline of the dominant kernel on compulsory bytes (frac <= 1), with the §8(d)
+    per-iteration figure and the whole section beside it (see the module docstring)."""
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    T = cfg["T"]
+    npx = cfg["B"] * cfg["H"] * cfg["W"]
+    es = 2 if cfg["dtype"] == "f16" else 4
+    plane = es * npx
+    if resident:
+        kname, kmean = "prop_resident_kernel", rest_ms
+        # reads: K normalised affinities (tap K/2 is recomputed), 2K offsets, conf', dep, p_1;
+        # writes: pred_inter[1..T-1] and pred
+        comp_planes = (K + 2 * K + 2 + 1) + (T - 1 + 1)
+        alg_iters = T - 1
+        kdesc = f"{kname} (iterations 2..{T} in one launch, invariant planes on chip)"
+    else:
+        kname, kmean = "prop_step_kernel", rest_ms / max(1, T - 1)
+        comp_planes = 4 + 3 * K  # p_in, conf', dep, K aff, 2K offsets read; p_out written
+        alg_iters = 1
+        kdesc = f"{kname} (one fused iteration)"
+    comp = comp_planes * plane
+    achieved = comp / (kmean * 1e-3) / 1e9
+    alg = es * (4 + 3 * K) * npx * alg_iters
+    sec = ((3 * K + 3) + (T + 3 * K + 5)) * plane
+    traffic = pmc_traffic(name, kname)
+    return {
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kdesc,
+        "bytes_basis": "compulsory bytes per launch (each plane the launch must read or write, once)",
+        "compulsory_bytes_per_launch": comp, "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5),
+        "traffic_over_compulsory": round(traffic / comp, 3) if traffic else None,
+        "alg_8d": {"bytes_per_launch": alg, "pixel_iterations_per_launch": npx * alg_iters,
+                   "achieved": round(alg / (kmean * 1e-3) / 1e9, 1),
+                   "frac": round(alg / (kmean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "note": "SURVEY 8(d) S*(4+3K) per pixel-iteration; credits the resident kernel with the "
+                           "invariant re-reads a per-iteration launch does, so it can exceed 1"},
+        "section": {"compulsory_bytes": sec, "achieved": round(sec / (ms_per_step * 1e-3) / 1e9, 1),
+                    "frac": round(sec / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "note": "whole section: raw head outputs read once, T pred_inter + pred + aff + offset + "
+                            "confidence written once, over ms_per_step"},
+    }
+
+
+def measure(name, steps, warmup, kernel_reps, world, rank, dev):
+    """Time one workload on every rank (barrier + synchronize on both sides, max over
+    ranks) and its dominant kernel; returns (result dict, inputs, synthetic arrays)."""
+    from nlspn_eccv20_amd.propagation import PropagationPlan
+    cfg = CONFIGS[name]
+    inputs, s = make_inputs(cfg, rank, dev)
+    plan = PropagationPlan(inputs["pred_init"], inputs["dep"], inputs["conf"], inputs["aff"], inputs["off"],
+                           inputs["gamma"], prop_time=cfg["T"], kernel=cfg["kernel"])
+    for _ in range(warmup):
+        plan.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        plan.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    mine = time.perf_counter() - t0
+    plan.check()  # a resident launch that aborted raises here (never silent)
+    spread = gather_over_ranks(mine, dev)
+    elapsed = max_over_ranks(mine, dev)
+    first_ms, rest_ms, resident = kernel_time(plan, inputs, cfg, kernel_reps, dev)
+    plan.check()
+    plan.close()
+    ms_per_step = 1e3 * elapsed / steps
+    out = {
+        "workload": f"{cfg['id']}: {cfg['desc']}",
+        "value": round(world * cfg["T"] * steps / elapsed, 1), "unit": "iters/s",
+        "ms_per_step": round(ms_per_step, 4), "ms_per_iter": round(ms_per_step / cfg["T"], 5),
+        "dtype": cfg["dtype"], "batch_per_gpu": cfg["B"], "global_batch": cfg["B"] * world,
+        "shard": list(shard_range(cfg["B"] * world, world, rank)),
+        "gpu_event_ms_per_step": round(ev0.elapsed_time(ev1) / steps, 4),
+        "rank_ms_per_step": [round(1e3 * x / steps, 4) for x in spread],
+        "roofline": roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step),
+    }
+    return out, inputs, s
+
+
 def backward_timing(inputs, cfg, steps):
     """Forward+backward of the whole section (training step of the propagation), with
     gradients for pred_init, confidence, the (B, 3K, H, W) head output and gamma."""
+    from nlspn_eccv20_amd.propagation import propagate
     K = cfg["kernel"][0] * cfg["kernel"][1] - 1
     pi = inputs["pred_init"].detach().clone().requires_grad_(True)
     cf = inputs["conf"].detach().clone().requires_grad_(True)
@@ -198,115 +316,137 @@ def gru_section_timing(inputs, cfg, steps, dev):
             "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration"}
 
 
-def cpu_baseline(cfg, s, reps):
-    from oracle import oracle as O  # test infrastructure: the CPU baseline leg only
-    threads = max(1, min(16, os.cpu_count() or 1))
-    O.set_threads(threads)
-    K = s["K"]
-    args = (s["pred_init"], s["dep"], s["conf"], s["off_aff"][:, 2 * K:], s["off_aff"][:, :2 * K], 0.5 * K)
-    kw = dict(kh=cfg["kernel"][0], kw=cfg["kernel"][1], prop_time=cfg["T"])
-    O.propagate(*args, **kw)  # warm-up
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _median_time(fn, reps, warm):
+    for _ in range(warm):
+        fn()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        O.propagate(*args, **kw)
+        fn()
         ts.append(time.perf_counter() - t0)
-    med = statistics.median(ts)
-    return {"value": cfg["T"] / med, "unit": "iters/s", "cores": threads, "kind": "port",
-            "sample": f"C oracle (oracle/nlspn_oracle.c, OpenMP {threads} threads, fp32) on the full "
-                      f"{cfg['id']} batch, 1 warm-up + median of {reps} whole propagations of T={cfg['T']}",
-            "ms_per_iter": 1e3 * med / cfg["T"]}
+    return statistics.median(ts)
+
+
+def cpu_baseline(reps, warm=2):
+    """SURVEY §8(d) CPU baseline on this host, rank 0, N=1: (i) the offset path through
+    the C oracle (kind "port": the reference has no CPU DCN) and (ii) the no-offset path
+    as the reference's own torch op sequence (nlspnmodel.py:209-224, oracle/torch_ref.py),
+    each at the C2 batch and the C1 batch (B=1) with all threads of this process's CPU
+    share, and at C1 with 1 thread; 2 warm-ups, median of `reps` whole sections."""
+    from oracle import oracle as O  # test infrastructure: the CPU baseline leg only
+    from oracle import torch_ref
+    host = os.cpu_count() or 1
+    # the GPU box gives one GPU's job a 16-core share (OMP_NUM_THREADS there); use it all
+    threads = max(1, min(host, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    legs = {}
+    for name in ("nyu", "nyu_b1"):
+        cfg = CONFIGS[name]
+        K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+        s = synth(cfg["B"], cfg["H"], cfg["W"], K, seed=7240, density=cfg["density"], max_depth=cfg["max_depth"])
+        a_off = (s["pred_init"], s["dep"], s["conf"], s["off_aff"][:, 2 * K:], s["off_aff"][:, :2 * K], 0.5 * K)
+        tt = {k: torch.from_numpy(s[k]) for k in ("pred_init", "dep", "conf")}
+        aff_t = torch.from_numpy(s["off_aff"][:, 2 * K:].copy())
+        for nth in ((threads, 1) if name == "nyu_b1" else (threads,)):
+            O.set_threads(nth)
+            torch.set_num_threads(nth)
+            med = _median_time(lambda: O.propagate(*a_off, prop_time=cfg["T"]), reps, warm)
+            legs[f"offset_{cfg['id']}_{nth}t"] = {"iters_per_s": round(cfg["T"] / med, 2),
+                                                   "ms_per_iter": round(1e3 * med / cfg["T"], 3)}
+            med = _median_time(lambda: torch_ref.propagate_noffset(tt["pred_init"], tt["dep"], tt["conf"], aff_t,
+                                                                   0.5 * K, prop_time=cfg["T"]), reps, warm)
+            legs[f"noffset_{cfg['id']}_{nth}t"] = {"iters_per_s": round(cfg["T"] / med, 2),
+                                                    "ms_per_iter": round(1e3 * med / cfg["T"], 3)}
+    head = legs[f"offset_C2_{threads}t"]
+    return {"value": head["iters_per_s"], "unit": "iters/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(), "host_logical_cpus": host,
+            "sample": (f"C2 workload (NYU B=8, K=8, T=18, fp32, learned offsets, TGASS) through the C oracle "
+                       f"(oracle/nlspn_oracle.c, OpenMP {threads} threads = this job's CPU share), {warm} warm-ups + "
+                       f"median of {reps} whole sections; legs: offset path (C oracle) and no-offset path (the "
+                       f"reference's torch op sequence, nlspnmodel.py:209-224) at C2 and C1 (B=1) with {threads} "
+                       f"threads and C1 with 1 thread"),
+            "ms_per_iter": head["ms_per_iter"], "legs": legs}
+
+
+def dry_run(a, world, rank):
+    """Launcher + sharding on CPU (gloo): every rank owns its shard of the global batch
+    and reports it; rank 0 prints one JSON line.  No GPU is touched."""
+    launch.init_from_env("gloo")
+    cfg = CONFIGS[a.config]
+    lo, hi = shard_range(cfg["B"] * world, world, rank)
+    t0 = time.perf_counter()
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    s = synth(hi - lo, 8, 8, K, seed=7240 + rank)
+    mine = time.perf_counter() - t0
+    shards = [None] * world
+    if world > 1:
+        dist.all_gather_object(shards, (rank, lo, hi, float(s["pred_init"].sum())))
+    else:
+        shards = [(rank, lo, hi, float(s["pred_init"].sum()))]
+    el = max_over_ranks(mine)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "config": cfg["id"], "global_batch": cfg["B"] * world,
+                          "shards": [[r, l, h] for r, l, h, _ in shards], "max_rank_s": el}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     a = parse()
-    cfg = CONFIGS[a.config]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, spawned here (the parent never initialises HIP)
+        sys.exit(launch.spawn_local(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    world, rank, local = launch.env_rank()
+    if a.dry_run:
+        return dry_run(a, world, rank)
+    if a.gpus != world:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
+              file=sys.stderr)
+    launch.init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    tdt = torch.float16 if cfg["dtype"] == "f16" else torch.float32
+    cfg = CONFIGS[a.config]
 
-    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
-    s = synth(cfg["B"], cfg["H"], cfg["W"], K, seed=7240 + rank, density=cfg["density"],
-              max_depth=cfg["max_depth"])
-    to = lambda x: torch.from_numpy(x).to(dev, tdt)  # noqa: E731
-    off_aff = to(s["off_aff"])
-    inputs = {"pred_init": to(s["pred_init"]), "dep": to(s["dep"]), "conf": to(s["conf"]),
-              "aff": off_aff[:, 2 * K:], "off": off_aff[:, :2 * K],
-              "gamma": torch.tensor([0.5 * K], device=dev)}
-    plan = PropagationPlan(inputs["pred_init"], inputs["dep"], inputs["conf"], inputs["aff"], inputs["off"],
-                           inputs["gamma"], prop_time=cfg["T"], kernel=cfg["kernel"])
-    for _ in range(a.warmup):
-        plan.replay()
-    torch.cuda.synchronize()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(a.steps):
-        plan.replay()
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    elapsed = max_over_ranks(elapsed, dev)
-
-    first_ms, rest_ms, resident = kernel_time(plan, inputs, cfg, a.kernel_reps, dev)
-    npx = cfg["B"] * cfg["H"] * cfg["W"]
-    es = 2 if cfg["dtype"] == "f16" else 4
-    # S*(4+3K) algorithmic bytes per pixel-iteration.  The dominant
-    # kernel is the resident kernel (T-1 pixel-iterations per pixel in one launch)
-    # when it applies, else the per-iteration step kernel (one per launch).
-    iters = cfg["T"] - 1 if resident else 1
-    kname = "prop_resident_kernel" if resident else "prop_step_kernel"
-    kmean = rest_ms if resident else rest_ms / max(1, cfg["T"] - 1)
-    bytes_per_launch = es * (4 + 3 * K) * npx * iters
-    achieved = bytes_per_launch / (kmean * 1e-3) / 1e9
-    traffic = pmc_traffic(a.config, kname)
-
-    ms_per_step = 1e3 * elapsed / a.steps
-    value = world * cfg["T"] * a.steps / elapsed
+    head, inputs, _ = measure(a.config, a.steps, a.warmup, a.kernel_reps, world, rank, dev)
     out = {
         "metric": baseline_metric(),
-        "value": round(value, 1), "unit": "iters/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(ms_per_step, 4), "ms_per_iter": round(ms_per_step / cfg["T"], 5),
+        "value": head["value"], "unit": "iters/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": head["ms_per_step"], "ms_per_iter": head["ms_per_iter"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
         "data": "synthetic (seeded; SURVEY §8d distribution, convex |N(0,1)| affinity, N(0,2^2) offsets)",
-        "config": {"workload": f"{cfg['id']}: {cfg['desc']}", "batch_per_gpu": cfg["B"],
-                   "global_batch": cfg["B"] * world, "H": cfg["H"], "W": cfg["W"], "K": K,
+        "config": {"workload": head["workload"], "batch_per_gpu": cfg["B"], "global_batch": cfg["B"] * world,
+                   "H": cfg["H"], "W": cfg["W"], "K": cfg["kernel"][0] * cfg["kernel"][1] - 1,
                    "kernel": list(cfg["kernel"]), "prop_time": cfg["T"],
                    "parallelism": f"dp{world} (batch shards, no collective)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": (f"{kname} (iterations 2..{cfg['T']} in one launch, invariant planes on chip)"
-                                if resident else f"{kname} (one fused iteration)"),
-                     "pixel_iterations_per_launch": npx * iters,
-                     "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5),
-                     # the HBM rate the kernel really drives (PMC bytes / its duration)
-                     "traffic_gbs": round(traffic / (kmean * 1e-3) / 1e9, 1) if traffic else None,
-                     "note": ("achieved credits SURVEY 8(d)'s per-iteration algorithmic bytes; this kernel reads "
-                              "the invariant planes once (see traffic), so frac > 1 measures on-chip reuse, "
-                              "not HBM bandwidth" if resident else None)},
-        "gpu_event_ms_per_step": round(gpu_ms / a.steps, 4),
+        "roofline": head["roofline"],
+        "gpu_event_ms_per_step": head["gpu_event_ms_per_step"],
+        "rank_ms_per_step": head["rank_ms_per_step"],
     }
     if cfg["dtype"] == "f32" and not a.no_backward:
         out["backward"] = backward_timing(inputs, cfg, a.backward_steps)
     if cfg["dtype"] == "f32" and cfg["kernel"] == (3, 3) and not a.no_gru:
         out["gru_section"] = gru_section_timing(inputs, cfg, a.backward_steps, dev)
+    del inputs
+    if not a.no_extra_configs:
+        out["configs"] = {}
+        for name in EXTRA:
+            if name == a.config:
+                continue
+            r, _, _ = measure(name, a.steps, a.warmup, a.kernel_reps, world, rank, dev)
+            out["configs"][CONFIGS[name]["id"]] = r
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, s, a.cpu_reps)
-    plan.close()
+        out["cpu_baseline"] = cpu_baseline(a.cpu_reps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

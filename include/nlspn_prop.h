@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define NLSPN_ABI_VERSION 2
+#define NLSPN_ABI_VERSION 3
 
 /* element type of every tensor argument (math is always fp32) */
 #define NLSPN_DTYPE_F32 0
@@ -55,6 +55,7 @@ extern "C" {
 #define NLSPN_EINVAL 1       /* bad shape / argument */
 #define NLSPN_EUNSUPPORTED 2 /* geometry or dtype without a kernel instantiation */
 #define NLSPN_EHIP 3         /* HIP runtime / launch error */
+#define NLSPN_EABORTED 4     /* a resident launch aborted (nlspn_resident_status) */
 
 /* Version of this ABI (NLSPN_ABI_VERSION). */
 int nlspn_abi_version(void);
@@ -294,6 +295,20 @@ int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, cons
  */
 int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf,
                           int *grid, int *block, int *lds_bytes);
+
+/*
+ * Sticky abort status of the resident path on the current device: 1 if a resident
+ * launch aborted since the last clear (a part polled past its spin limit, i.e. the
+ * grid was not co-resident — e.g. a concurrent resident launch from another
+ * process; launches from this process are serialised per device across streams).
+ * Such a launch fills the outputs it had not written with NaN.  Reads a
+ * host-mapped word the kernel writes: never synchronises, so the host sees an
+ * abort once the launch has finished.  Sets nlspn_last_error (NLSPN_EABORTED).
+ * clear != 0 resets the word after reading it.  Replaces nothing in the
+ * reference, whose kernels only printf launch errors (.cuh:348-352); the torch
+ * layer raises RuntimeError on it, as c10::Error surfaces in the reference.
+ */
+int nlspn_resident_status(int clear);
 
 #ifdef __cplusplus
 }

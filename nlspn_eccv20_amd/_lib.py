@@ -22,7 +22,7 @@ DTYPE_F32, DTYPE_F16 = 0, 1
 AFF_KINDS = {"AS": 0, "ASS": 1, "TC": 2, "TGASS": 3}
 PRESERVE_INPUT, ALWAYS_CLIP = 0x1, 0x2
 OFF_INSERTED, OFF_RAW = 0, 1
-EINVAL, EUNSUPPORTED, EHIP = 1, 2, 3
+EINVAL, EUNSUPPORTED, EHIP, EABORTED = 1, 2, 3, 4
 
 _vp, _i, _u, _i64, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint, ctypes.c_int64, ctypes.c_size_t
 _fp = ctypes.POINTER(ctypes.c_float)
@@ -57,6 +57,7 @@ SIGNATURES = {
     "nlspn_time_propagate": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _i, _i, _i, _i, _i, _i, _i, _u, _i, _vp, _vp, _vp, _vp]),
     "nlspn_resident_config": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "nlspn_resident_status": (_i, [_i]),
     "nlspn_affinity_normalize_backward": (_i, [_i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
 }
 
@@ -93,6 +94,20 @@ def check(rc: int) -> None:
     if rc != 0:
         msg = get().nlspn_last_error().decode(errors="replace")
         raise NlspnError(rc, msg)
+
+
+def check_resident(device=None) -> None:
+    """Raise NlspnError (a RuntimeError) if a resident launch on `device` (default: the
+    current one) aborted since the last check; clears the sticky word.  No device sync:
+    an abort is seen once the aborted launch has finished."""
+    lib = get()
+    if device is None:
+        hit = lib.nlspn_resident_status(1)
+    else:
+        with torch.cuda.device(device):
+            hit = lib.nlspn_resident_status(1)
+    if hit:
+        raise NlspnError(EABORTED, lib.nlspn_last_error().decode(errors="replace"))
 
 
 def header_symbols() -> list[str]:

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -187,6 +188,71 @@ int device_cus() {
     return cached[dev];
 }
 
+// Per-device state of the resident path.
+//  * status: a host-mapped sticky word the resident kernel sets when a launch
+//    aborts (nlspn_resident.h); nlspn_resident_status reads it with no device sync.
+//  * res_guard: the resident kernel needs every workgroup co-resident, so two of
+//    its launches must never run at once on one device.  Resident launches are
+//    serialised across streams: a launch on a stream other than the previous
+//    resident launch's waits for that launch's event.  (Skipped while a stream is
+//    being captured: a plan re-applies the guard when it is launched.)
+struct DevState {
+    std::mutex m;
+    unsigned *host_status = nullptr, *dev_status = nullptr;
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool init = false;
+};
+constexpr int kMaxDevices = 64;
+DevState g_dev[kMaxDevices];
+
+DevState *dev_state() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    DevState &d = g_dev[dev];
+    std::lock_guard<std::mutex> lk(d.m);
+    if (!d.init) {
+        void *h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+            void *dp = nullptr;
+            if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess) {
+                d.host_status = static_cast<unsigned *>(h);
+                d.dev_status = static_cast<unsigned *>(dp);
+                *d.host_status = 0u;
+            } else {
+                (void)hipHostFree(h);
+            }
+        }
+        d.init = true;
+    }
+    return &d;
+}
+
+bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+int res_guard_before(hipStream_t s) {
+    if (stream_capturing(s)) return NLSPN_OK;
+    DevState *d = dev_state();
+    if (!d) return NLSPN_OK;
+    std::lock_guard<std::mutex> lk(d->m);
+    if (d->last_ev && d->last_stream != s) NLSPN_HIP_TRY(hipStreamWaitEvent(s, d->last_ev, 0));
+    return NLSPN_OK;
+}
+
+int res_guard_after(hipStream_t s) {
+    if (stream_capturing(s)) return NLSPN_OK;
+    DevState *d = dev_state();
+    if (!d) return NLSPN_OK;
+    std::lock_guard<std::mutex> lk(d->m);
+    if (!d->last_ev) NLSPN_HIP_TRY(hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
+    NLSPN_HIP_TRY(hipEventRecord(d->last_ev, s));
+    d->last_stream = s;
+    return NLSPN_OK;
+}
+
 struct ResPlan {
     const void *fn = nullptr;
     unsigned grid = 0, block = 0;
@@ -245,8 +311,10 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     P.block = (unsigned)nt;
     P.lds = lds;
     P.sync_bytes = ((G + 1) * 4 + 15) / 16 * 16;
+    DevState *ds = dev_state();
     P.a = ResArgs{conf_eff, (flags & kPreserve) ? dep : nullptr, aff_norm, off_raw, pred_inter, pred,
-                  static_cast<unsigned *>(workspace), off_bs, B, H, W, T, g, (int)wh_max, flags, 0u};
+                  static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, B, H, W, T, g,
+                  (int)wh_max, flags, 0u};
     if (const char *d = getenv("NLSPN_RES_DBG")) P.a.dbg = (unsigned)atoi(d);
     return true;
 }
@@ -255,12 +323,15 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
     if (g_rec) g_rec->push_back(LaunchRec{P.fn, dim3(P.grid), dim3(P.block), P.lds, true, StepArgs{}, P.a});
+    int rc = res_guard_before(s);
+    if (rc) return rc;
     void *args[] = {&P.a};
     if (e0)
         NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s, e0, e1, 0));
     else
         NLSPN_HIP_TRY(hipLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s));
-    return check_launch("nlspn_propagate resident");
+    if ((rc = check_launch("nlspn_propagate resident"))) return rc;
+    return res_guard_after(s);
 }
 
 // ------------------------------------------------------- affinity-normalisation dispatch
@@ -486,6 +557,7 @@ struct nlspn_plan {
     hipGraphExec_t exec = nullptr;
     std::vector<LaunchRec> recs;
     bool direct = false;
+    bool resident = false;  // holds a resident launch: res_guard applies around replays
 };
 
 int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -526,6 +598,7 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
     p->exec = ge;
     const char *env = getenv("NLSPN_PLAN_GRAPH");
     p->direct = recs.size() <= kPlanDirectMax && !(env && env[0] == '1');
+    for (const LaunchRec &r : recs) p->resident = p->resident || r.resident;
     p->recs = std::move(recs);
     *plan = p;
     return NLSPN_OK;
@@ -533,13 +606,18 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
 
 int nlspn_plan_launch(nlspn_plan_t plan, void *stream) {
     if (!plan) return fail(NLSPN_EINVAL, "plan is null");
+    hipStream_t s = as_stream(stream);
+    int rc = NLSPN_OK;
     if (!plan->direct) {
-        NLSPN_HIP_TRY(hipGraphLaunch(plan->exec, as_stream(stream)));
-        return NLSPN_OK;
+        if (plan->resident && (rc = res_guard_before(s))) return rc;
+        NLSPN_HIP_TRY(hipGraphLaunch(plan->exec, s));
+        return plan->resident ? res_guard_after(s) : NLSPN_OK;
     }
     for (LaunchRec &r : plan->recs) {
         void *args[] = {r.resident ? static_cast<void *>(&r.ra) : static_cast<void *>(&r.sa)};
-        NLSPN_HIP_TRY(hipLaunchKernel(r.fn, r.grid, r.block, args, r.lds, as_stream(stream)));
+        if (r.resident && (rc = res_guard_before(s))) return rc;
+        NLSPN_HIP_TRY(hipLaunchKernel(r.fn, r.grid, r.block, args, r.lds, s));
+        if (r.resident && (rc = res_guard_after(s))) return rc;
     }
     return check_launch("nlspn_plan_launch");
 }
@@ -690,8 +768,8 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     if (grad_aff_bstride < 0 || grad_off_bstride < 0 || (grad_aff_bstride && grad_aff_bstride < (long long)K * HW) ||
         (grad_off_bstride && grad_off_bstride < 2LL * K * HW))
         return fail(NLSPN_EINVAL, "gradient batch strides below K*H*W / 2K*H*W (0 = contiguous)");
-    if (grad_aff_bstride % 4 != 0 || grad_off_bstride % 4 != 0)
-        return fail(NLSPN_EINVAL, "gradient batch strides must be multiples of 4 elements");
+    // (no alignment requirement: every grad_aff_raw / grad_off_raw access is a
+    // 4-byte buffer load/store, nlspn_backward.h)
     hipStream_t s = as_stream(stream);
     float *ws = static_cast<float *>(workspace);
     float *gf[2] = {ws, ws + N};
@@ -907,6 +985,18 @@ int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, cons
     *rest_ms = (float)(r / reps);
     if (resident) *resident = res;
     return NLSPN_OK;
+}
+
+int nlspn_resident_status(int clear) {
+    DevState *d = dev_state();
+    if (!d || !d->host_status) return 0;
+    const unsigned v = __atomic_load_n(d->host_status, __ATOMIC_ACQUIRE);
+    if (v && clear) __atomic_store_n(d->host_status, 0u, __ATOMIC_RELEASE);
+    if (v)
+        fail(NLSPN_EABORTED,
+             "a resident propagation launch on this device aborted (a part waited past its spin limit: the grid "
+             "was not co-resident); its outputs were filled with NaN");
+    return v ? 1 : 0;
 }
 
 int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf, int *grid,

@@ -37,9 +37,12 @@
 //
 // Residency: G = B * g workgroups (g parts per image), at most one per CU (the
 // dynamic LDS request exceeds half a CU's LDS) and G <= CU count, so the whole
-// grid is resident.  Every spin is bounded: on timeout a part raises the abort
-// word (sync[G]) and every part exits; outputs are then invalid and the abort
-// word stays set for the host to inspect.
+// grid is resident (the host serialises resident launches of one device across
+// streams, nlspn_capi.hip res_guard).  Every spin is bounded: on timeout a part
+// raises the abort word (sync[G]) and the device's host-mapped sticky status word
+// (ResArgs::status, read by nlspn_resident_status without a device sync), and every
+// part that sees the abort fills its own quads of the planes it has not written
+// (and pred) with NaN before it exits: an aborted launch never looks valid.
 #pragma once
 
 #include "nlspn_common.h"
@@ -57,13 +60,15 @@ struct ResArgs {
     void *pred_inter;   // T x B planes: iteration t reads plane t-1, writes plane t
     void *pred;         // B planes: max(p_T, 0) (nlspnmodel.py:375-377)
     unsigned *sync;     // [G] progress words, [G] abort word; zeroed before every launch
+    unsigned *status;   // host-mapped sticky abort flag of the device (nlspn_resident_status), or null
     long long off_bs;   // elements
     int B, H, W, T;
     int g;              // parts (workgroups) per image
     int wh_max;         // LDS window rows allocated per buffer
     unsigned flags;
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
-                        // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid)
+                        // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid),
+                        // 32 part 0 aborts at t = 2 (tests of the error reporting)
 };
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
@@ -115,9 +120,13 @@ template <> struct ResVec<__half> {
         const f16x4 q = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, AUX);
     }
+    // one element by a 4-byte load of its aligned dword (the hand-off table of
+    // MI355X_MICROARCH.md validates sc1 loads of 4/8/16 bytes, not 2), half selected
     template <unsigned AUX>
     static __device__ __forceinline__ float load1(rsrc_t r, unsigned vo, unsigned so) {
-        return (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, AUX));
+        const unsigned at = vo + so;
+        const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(r, at & ~3u, 0u, AUX);
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)((at & 2u) ? (w >> 16) : (w & 0xffffu)));
     }
 };
 
@@ -307,6 +316,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     T *p_out_all = static_cast<T *>(a.pred_inter);
     const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
 
+    int t_abort = 0;
     for (int t = 1; t < a.T; ++t) {
         // The tap geometry depends only on the (invariant) coordinates, so the
         // compiler would hoist all 32 taps' weights and addresses out of this loop
@@ -319,6 +329,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
         asm volatile("" : "+v"(tb));
+        // and the thread's LDS affinity rows: without this the compiler keeps the ten
+        // row addresses live across the loop and spills them to scratch
+        int tq = tid;
+        asm volatile("" : "+v"(tq));
 
         unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                       ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
@@ -326,7 +340,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- wait until every part this one reads has finished iteration t-1
         if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
-            bool fail = false;
+            bool fail = (a.dbg & 32u) && blockIdx.x == 0;  // test hook: part 0 of image 0 aborts
             for (int base = jlo; base <= jhi && !fail; base += 64) {
                 const int jj = base + lane;
                 for (;;) {
@@ -346,10 +360,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (fail && lane == 0) {
                 ctl[0] = 1;
                 __hip_atomic_store(&sync[G], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
-        if (ctl[0]) return;
+        if (ctl[0]) {  // aborted: poison what this part has not produced (below), then exit
+            t_abort = t;
+            break;
+        }
         if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
 
         // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
@@ -400,11 +418,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (k == REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
-                    const float4 ar = akl[K * NT + tid];
+                    const float4 ar = akl[K * NT + tq];
                     const float *c = &fwin[(y - rlo) * WW + x0 + RX];
                     acc[0] += c[0] * ar.x; acc[1] += c[1] * ar.y; acc[2] += c[2] * ar.z; acc[3] += c[3] * ar.w;
                 }
-                const float4 a4 = akl[k * NT + tid];
+                const float4 a4 = akl[k * NT + tq];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -430,11 +448,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll 1
                     for (int k = 0; k < K; ++k) {
                         if (k == REF) {
-                            const float4 ar = akl[K * NT + tid];
+                            const float4 ar = akl[K * NT + tq];
                             const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
                             s += fwin[(y - rlo) * WW + x0 + e + RX] * arv[e];
                         }
-                        const float4 a4 = akl[k * NT + tid];
+                        const float4 a4 = akl[k * NT + tq];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
                         const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
                         const float h_im = (float)(y - PH + i) +
@@ -501,7 +519,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
         // this iteration is done: the barrier above), as the next staging would load it
         if (t < a.T - 1 && active && !(a.dbg & 2u)) {
-            const float4 cw = akl[(K + 1) * NT + tid];
+            const float4 cw = akl[(K + 1) * NT + tq];
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
             if (has_conf) {
                 f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
@@ -512,6 +530,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
             fwinB[li + 2] = f.w;
         }
+    }
+    if (t_abort && active) {  // an aborted launch never looks valid: NaN in every unwritten plane
+        const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+        for (int tt = t_abort; tt < a.T; ++tt)
+            ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * N + b * HW), vpix, 0u, qn);
+        ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, qn);
     }
 }
 

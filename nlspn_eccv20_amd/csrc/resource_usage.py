@@ -1,26 +1,63 @@
 #!/usr/bin/env python3
-"""Summarise hipcc -Rpass-analysis=kernel-resource-usage remarks as a table."""
+"""Per-kernel resource usage from hipcc -Rpass-analysis=kernel-resource-usage remarks.
+
+The Makefile writes the remarks of every compile to build/csrc/*.ru.txt; `parse`
+turns them into {mangled name: {VGPRs, AGPRs, ScratchSize, Occupancy, ...}} and
+the CLI prints a table (optionally filtered by a substring of the demangled name).
+tests/test_resource_usage_cpu.py uses `load_build` to assert that the step and
+resident kernels do not spill to scratch.
+
+usage: resource_usage.py [FILTER]
+"""
+import glob
+import os
 import re
 import subprocess
 import sys
 
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-       "-ffp-contract=off", "-Rpass-analysis=kernel-resource-usage", "-o", "/tmp/nlspn_ru.so", "nlspn_capi.hip"]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
-rows, cur = [], None
-for line in out.splitlines():
-    m = re.search(r"Function Name: (\S+)", line)
-    if m:
-        cur = {"name": m.group(1)}
-        rows.append(cur)
-        continue
-    m = re.search(r"remark:\s+(VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]|TotalSGPRs): (\d+)", line)
-    if m and cur is not None:
-        cur[m.group(1).split()[0]] = int(m.group(2))
-filt = sys.argv[1] if len(sys.argv) > 1 else ""
-for r in rows:
-    if filt in r["name"]:
-        dem = subprocess.run(["c++filt", r["name"]], capture_output=True, text=True).stdout.strip()
-        dem = dem.replace("nlspn::", "").replace("(StepArgs)", "").replace("void ", "")
-        print(f"{dem[:90]:90s} vgpr={r.get('VGPRs')} sgpr={r.get('TotalSGPRs')} scratch={r.get('ScratchSize')} "
-              f"occ={r.get('Occupancy')} lds={r.get('LDS')}")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.normpath(os.path.join(_HERE, "..", "..", "build", "csrc"))
+_FIELD = re.compile(r"remark:\s+(VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                    r"LDS Size \[bytes/block\]|TotalSGPRs|SGPRs Spill|VGPRs Spill): (\d+)")
+
+
+def parse(text: str) -> dict:
+    rows, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = rows.setdefault(m.group(1), {})
+            continue
+        m = _FIELD.search(line)
+        if m and cur is not None:
+            key = m.group(1) if m.group(1) in ("SGPRs Spill", "VGPRs Spill") else m.group(1).split()[0]
+            cur[key] = int(m.group(2))
+    return rows
+
+
+def load_build(build_dir: str = BUILD_DIR) -> dict:
+    rows = {}
+    for p in sorted(glob.glob(os.path.join(build_dir, "*.ru.txt"))):
+        with open(p) as f:
+            rows.update(parse(f.read()))
+    return rows
+
+
+def demangle(names):
+    out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")
+    return [o.replace("nlspn::", "").replace("void ", "") for o in out[:len(names)]]
+
+
+def main():
+    filt = sys.argv[1] if len(sys.argv) > 1 else ""
+    rows = load_build()
+    names = sorted(rows)
+    for n, d in zip(names, demangle(names)):
+        if filt in d:
+            r = rows[n]
+            print(f"{d[:100]:100s} vgpr={r.get('VGPRs')} sgpr={r.get('TotalSGPRs')} scratch={r.get('ScratchSize')} "
+                  f"occ={r.get('Occupancy')} lds={r.get('LDS')}")
+
+
+if __name__ == "__main__":
+    main()

@@ -311,6 +311,7 @@ class _PropagateFn(torch.autograd.Function):
         args, _ = _propagate_args(pred_init, dep, confidence, aff, offset, gamma, kernel, prop_time, affinity,
                                   preserve_input, always_clip, outs)
         with torch.cuda.device(pred_init.device):
+            _lib.check_resident()  # an earlier resident launch that aborted raises here
             _lib.check(_lib.get().nlspn_propagate(*args, _stream(pred_init.device)))
         ctx.cfg = (kh, kw, int(prop_time), affinity, preserve_input, always_clip)
         ctx.save_for_backward(pred_init, dep, confidence, aff, offset, gamma, outs["pred_inter"], outs["aff"],
@@ -364,11 +365,19 @@ def _packed_head(aff, offset):
     """The contiguous (B, 3K, H, W) tensor that `offset` (planes 0..2K-1) and `aff`
     (planes 2K..3K-1) are slices of, when it requires grad (nlspnmodel.py:304-305 slice
     the head output so): autograd then gets ONE gradient for it instead of two
-    zero-filled full-size ones summed.  None otherwise."""
+    zero-filled full-size ones summed.  None otherwise — in particular when either
+    slice does not itself require grad (e.g. it was cut off under no_grad), or the
+    slices' strides differ from the base's.  Note: the gradient then flows to the
+    base directly, so hooks / retain_grad() registered on the two slices do not fire."""
     if offset is None or aff._base is None or offset._base is not aff._base:
         return None
     base = aff._base
     if not base.requires_grad or base.dim() != 4 or not base.is_contiguous() or base.dtype != torch.float32:
+        return None
+    # slices taken under no_grad report requires_grad but have no grad_fn: not in the graph
+    if not (aff.requires_grad and offset.requires_grad) or aff.grad_fn is None or offset.grad_fn is None:
+        return None
+    if aff.stride() != base.stride() or offset.stride() != base.stride():
         return None
     B, K = aff.shape[0], aff.shape[1]
     HW = aff.shape[2] * aff.shape[3]
@@ -401,9 +410,11 @@ def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: 
 
 
 class PropagationPlan:
-    """propagate() captured once into a native hipGraph (nlspn_plan_create) over fixed
-    input/output buffers; replay() re-runs the whole section with one hipGraphLaunch.
-    Refill the input tensors in place between replays; γ is read on the device."""
+    """propagate() captured once (nlspn_plan_create) over fixed input/output buffers;
+    replay() re-runs the whole section (the recorded launches re-issued directly, or
+    one hipGraphLaunch).  Refill the input tensors in place between replays; γ is
+    read on the device.  Resident launches of one device are serialised across
+    streams by the library; check() raises if one aborted."""
 
     def __init__(self, pred_init, dep, confidence, aff, offset, gamma, *, prop_time=18, affinity="TGASS",
                  kernel=(3, 3), preserve_input=True, always_clip=False, return_offset=True):
@@ -421,10 +432,17 @@ class PropagationPlan:
 
     def replay(self) -> dict:
         with torch.cuda.device(self.device):
+            _lib.check_resident()  # an earlier resident launch that aborted raises here
             _lib.check(self._lib.nlspn_plan_launch(self._plan, _stream(self.device)))
         o = self.outputs
         return {"pred": o["pred"], "pred_inter": list(o["pred_inter"].unbind(0)), "offset": o["offset"],
                 "aff": o["aff"], "confidence": o["confidence"], "pred_inter_tensor": o["pred_inter"]}
+
+    def check(self) -> None:
+        """Wait for this device's queued work, then raise RuntimeError if a resident
+        launch aborted (its outputs are NaN-filled; see nlspn_resident_status)."""
+        torch.cuda.synchronize(self.device)
+        _lib.check_resident(self.device)
 
     def close(self) -> None:
         if getattr(self, "_plan", None) is not None and self._plan.value:

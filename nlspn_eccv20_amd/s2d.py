@@ -32,7 +32,8 @@ def _run(dep, w1, b1, w2, b2, want_pyr):
     for n, t in (("dep", dep), ("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2)):
         if not t.is_cuda or t.dtype != torch.float32:
             raise RuntimeError(f"{n} must be a float32 CUDA tensor")
-    if tuple(w1.shape[:2]) != (8, 6) or tuple(w2.shape[:2]) != (16, 8) or b1.numel() != 8 or b2.numel() != 16:
+    if (tuple(w1.shape) != (8, 6, 1, 1) or tuple(w2.shape) != (16, 8, 1, 1) or b1.numel() != 8
+            or b2.numel() != 16):
         raise RuntimeError("pool_convs must be Conv2d(6, 8, 1) and Conv2d(8, 16, 1) (nlspnmodel.py:423-426)")
     dep, w1, b1, w2, b2 = (t.contiguous() for t in (dep, w1, b1, w2, b2))
     out = torch.empty((B, 17, H, W), dtype=torch.float32, device=dep.device)

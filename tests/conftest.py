@@ -45,3 +45,22 @@ def oracle():
     from oracle import oracle as O
     O.build()
     return O
+
+
+@pytest.fixture
+def record_metric():
+    """Append a measured parity number to gpurun_out/metrics.jsonl (merged back from the
+    GPU box), so tolerances can be tightened from evidence."""
+    import json
+    import time
+
+    def rec(name, value):
+        d = os.path.join(ROOT, "gpurun_out")
+        try:
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, "metrics.jsonl"), "a") as f:
+                f.write(json.dumps({"name": name, "value": float(value), "time": time.time()}) + "\n")
+        except OSError:
+            pass
+        print(f"[metric] {name} = {value:.3e}")
+    return rec

@@ -28,7 +28,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_workspace():
     lib = _lib.get()
-    assert lib.nlspn_abi_version() == 2
+    assert lib.nlspn_abi_version() == 3
     # resident kernel progress words (a 16-B multiple: one word per workgroup + abort word)
     assert lib.nlspn_workspace_bytes(0, 8, 228, 304) == 4096
     assert lib.nlspn_resident_config(0, 8, 228, 304, 3, 3, 18, 1, None, None, None) == 0  # no GPU here

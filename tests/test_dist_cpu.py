@@ -62,3 +62,30 @@ def test_gloo_two_ranks_shards_reassemble():
     equal, tmax = q.get(timeout=5)
     assert equal
     assert tmax == 2.0
+
+
+def test_bench_launcher_spawns_ranks_dry_run():
+    """bench.py --gpus 2 with no torchrun environment spawns 2 ranks itself
+    (launch.spawn_local); --dry-run runs the launcher + sharding path on CPU (gloo):
+    n_gpus = 2 and each rank owns its contiguous shard of the 2x global batch
+    (C4's form: KITTI B=4 per GPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--config", "kitti"], capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["global_batch"] == 8
+    assert line["shards"] == [[0, 0, 4], [1, 4, 8]]
+
+
+def test_spawn_local_propagates_failure():
+    import sys
+    from nlspn_eccv20_amd.launch import spawn_local
+    code = "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' else 0)"
+    assert spawn_local(2, [sys.executable, "-c", code], timeout=60) == 3
+    assert spawn_local(2, [sys.executable, "-c", "import os; assert os.environ['WORLD_SIZE'] == '2'"],
+                       timeout=60) == 0

@@ -104,10 +104,18 @@ def test_module_trains(oracle):
     assert m.aff_scale_const.grad is not None and m.w.grad is None
 
 
-def test_packed_head_gradient_equals_separate_slices():
+@pytest.mark.parametrize("B,H,W,kernel,affinity", [
+    (2, 48, 64, (3, 3), "TGASS"),
+    (1, 48, 64, (3, 3), "TGASS"),   # B=1: _planes returns C*H*W, not a real batch stride
+    (2, 37, 51, (3, 3), "AS"),      # W % 4 != 0: the scalar (non-vec) kernels
+    (2, 40, 60, (3, 3), "TC"),
+    (2, 33, 45, (5, 5), "TGASS"),   # odd H, W: packed batch stride not 16-B aligned
+    (1, 23, 37, (1, 17), "ASS"),
+])
+def test_packed_head_gradient_equals_separate_slices(B, H, W, kernel, affinity):
     """offset/aff sliced from one (B, 3K, H, W) head output get ONE packed gradient
     (propagation._packed_head); it equals the gradients of separate leaf tensors."""
-    K, B, H, W, T = 8, 2, 48, 64, 6
+    K, T = kernel[0] * kernel[1] - 1, 6
     s = synth(B, H, W, K, seed=4, density=0.05, off_sigma=2.0)
     t = lambda x, rg=True: torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(rg)  # noqa: E731
     gp = torch.randn((B, 1, H, W), device=DEV)
@@ -118,8 +126,10 @@ def test_packed_head_gradient_equals_separate_slices():
             off, aff = oa[:, :2 * K], oa[:, 2 * K:]
         else:
             off, aff = t(s["off_aff"][:, :2 * K]), t(s["off_aff"][:, 2 * K:])
-        g = torch.tensor([4.0], device=DEV, requires_grad=True)
-        o = propagate(t(s["pred_init"]), t(s["dep"], False), t(s["conf"]), aff, off, g, prop_time=T)
+        g = torch.tensor([4.0 if affinity != "TC" else float(K)], device=DEV,
+                         requires_grad=affinity == "TGASS")
+        o = propagate(t(s["pred_init"]), t(s["dep"], False), t(s["conf"]), aff, off, g, prop_time=T,
+                      kernel=kernel, affinity=affinity)
         torch.autograd.backward(o["pred"], gp)
         torch.cuda.synchronize()
         grads.append(oa.grad if packed else torch.cat([off.grad, aff.grad], 1))

@@ -201,6 +201,41 @@ def test_fp16_vs_fp32_oracle(oracle):
     assert err < 1e-2, err
 
 
+def test_c5_full_size_fp16_vs_fp32_oracle(oracle, record_metric):
+    """Config C5 at full size (BASELINE.json configs[4]): NYU 228x304, B=16, K=16 (1x17),
+    T=36, fp16 storage, against the fp32 oracle on the same fp16-rounded inputs.
+    Bar: RMSE <= 1e-2 on depth in [0, 10]; the measured value is
+    recorded (gpurun_out/metrics.jsonl)."""
+    s = synth(16, 228, 304, 16, seed=7240, density=500 / (228 * 304))
+    for k in ("pred_init", "dep", "conf", "off_aff"):
+        s[k] = s[k].astype(np.float16).astype(np.float32)
+    o = gpu_propagate(s, gamma=8.0, kernel=(1, 17), T=36, dtype=torch.float16)
+    oracle.set_threads(16)
+    e = oracle_propagate(oracle, s, gamma=8.0, kernel=(1, 17), T=36)
+    err = rmse(host(o["pred"]), e["pred"])
+    err_inter = rmse(host(o["pred_inter_tensor"]), e["pred_inter"])
+    record_metric("c5_full_fp16_rmse_pred", err)
+    record_metric("c5_full_fp16_rmse_pred_inter", err_inter)
+    assert err <= 1e-2, err
+    assert err_inter <= 1e-2, err_inter
+    p = host(o["pred"])
+    assert np.isfinite(p).all() and p.min() >= 0 and p.max() <= 10.0
+
+
+def test_c1_batch1_vs_oracle(oracle, record_metric):
+    """Config C1's workload (NYU 228x304, K=8, T=18, B=1) through the HIP path vs the
+    oracle: B=1 gets 256 parts of one image in the resident kernel."""
+    s = synth(1, 228, 304, 8, seed=7240, density=500 / (228 * 304))
+    o = gpu_propagate(s, gamma=4.0)
+    e = oracle_propagate(oracle, s, gamma=4.0)
+    err = rmse(host(o["pred"]), e["pred"])
+    record_metric("c1_b1_rmse_pred", err)
+    assert err <= 1e-4, err
+    np.testing.assert_allclose(host(o["pred_inter_tensor"]), e["pred_inter"], rtol=0, atol=1e-3)
+    np.testing.assert_array_equal(host(o["offset"]), e["offset"])
+    np.testing.assert_array_equal(host(o["confidence"]), e["confidence"])
+
+
 def test_plan_replay_equals_eager():
     s = synth(3, 40, 64, 8, seed=8)
     K = 8

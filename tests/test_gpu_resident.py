@@ -185,3 +185,62 @@ def test_time_propagate_reports_resident():
     os.environ.pop("NLSPN_RESIDENT", None)
     assert res.value == 1 and first.value > 0 and rest.value > 0
     plan.close()
+
+
+def test_two_plans_on_two_streams_bit_exact():
+    """Two resident plans replayed concurrently on two streams of one device: the
+    library serialises resident launches across streams (co-residency), so every
+    replay is bit-exact and nothing aborts (never silent garbage)."""
+    inp_a, _ = _inputs(8, 228, 304, seed=21)
+    inp_b, _ = _inputs(8, 228, 304, seed=22)
+    with _env("1"):
+        ref_a = propagate(*inp_a, prop_time=18)["pred_inter_tensor"].clone()
+        ref_b = propagate(*inp_b, prop_time=18)["pred_inter_tensor"].clone()
+        torch.cuda.synchronize()
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        with torch.cuda.stream(s1):
+            pa = PropagationPlan(*inp_a, prop_time=18)
+        with torch.cuda.stream(s2):
+            pb = PropagationPlan(*inp_b, prop_time=18)
+        torch.cuda.synchronize()
+        for i in range(12):
+            with torch.cuda.stream(s1):
+                oa = pa.replay()
+            with torch.cuda.stream(s2):
+                ob = pb.replay()
+            if i % 4 == 3:
+                torch.cuda.synchronize()
+                assert torch.equal(oa["pred_inter_tensor"], ref_a), f"plan A replay {i}"
+                assert torch.equal(ob["pred_inter_tensor"], ref_b), f"plan B replay {i}"
+        pa.check()
+        pb.check()
+        pa.close()
+        pb.close()
+
+
+def test_aborted_launch_raises_and_poisons():
+    """A resident launch that aborts (forced here: NLSPN_RES_DBG=32 makes part 0 abort) sets
+    the device's sticky status: the next call / check() raises RuntimeError, and the
+    planes the aborted parts never wrote hold NaN, not plausible depths."""
+    inp, _ = _inputs(8, 228, 304, seed=5)
+    old = os.environ.get("NLSPN_RES_DBG")
+    os.environ["NLSPN_RES_DBG"] = "32"
+    try:
+        with _env("1"):
+            plan = PropagationPlan(*inp, prop_time=18)
+        o = plan.replay()
+        with pytest.raises(RuntimeError, match="aborted"):
+            plan.check()
+        assert torch.isnan(o["pred_inter_tensor"][1:]).any()
+        plan.close()
+    finally:
+        if old is None:
+            os.environ.pop("NLSPN_RES_DBG", None)
+        else:
+            os.environ["NLSPN_RES_DBG"] = old
+    _lib.check_resident()  # the sticky word was cleared by the raise
+    with _env("1"):
+        o = propagate(*inp, prop_time=18)
+    torch.cuda.synchronize()
+    _lib.check_resident()
+    assert not torch.isnan(o["pred"]).any()

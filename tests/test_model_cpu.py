@@ -125,3 +125,16 @@ def test_registry():
     assert M.get(make_args()) is NLSPNModel
     with pytest.raises(NotImplementedError):
         M.get(make_args(model_name="Other"))
+
+
+def test_dataparallel_wraps_model():
+    """The reference wraps the model in nn.DataParallel (src/main.py:366); the drop-in
+    must construct under it with the same state_dict (module.-prefixed) and expose the
+    propagation module.  (Multi-GPU scatter itself: sharding.propagate_sharded / bench.)"""
+    m = NLSPNModel(make_args())
+    dp = torch.nn.DataParallel(m)
+    keys = set(dp.state_dict())
+    assert keys == {"module." + k for k in m.state_dict()}
+    dp2 = torch.nn.DataParallel(NLSPNModel(make_args()))
+    dp2.load_state_dict(dp.state_dict(), strict=True)
+    assert dp.module is m

@@ -1,0 +1,58 @@
+"""CPU: the hot kernels compile without scratch spills.
+
+The Makefile saves hipcc's -Rpass-analysis=kernel-resource-usage remarks of every
+compile (build/csrc/*.ru.txt).  A spill inside the resident kernel's iteration loop
+costs scratch round trips every iteration, so a spill coming back must fail a test,
+not hide in the build log.  If the library has not been built here, the resident
+translation unit (seconds) is compiled with the remarks on the spot.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "nlspn_eccv20_amd", "csrc")
+sys.path.insert(0, CSRC)
+import resource_usage as RU  # noqa: E402
+
+HOT = ("prop_resident_kernel", "prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
+
+
+def _rows():
+    rows = RU.load_build()
+    if any("prop_resident_kernel" in n for n in rows):
+        return rows
+    out = subprocess.run(
+        ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+         "-fno-slp-vectorize", "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/nlspn_ru_test.o",
+         os.path.join(CSRC, "nlspn_kern_resident.hip")], capture_output=True, text=True, cwd=CSRC)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return RU.parse(out.stderr)
+
+
+def test_hot_kernels_have_no_scratch():
+    rows = _rows()
+    hot = {n: r for n, r in rows.items() if any(h in n for h in HOT)}
+    assert any("prop_resident_kernel" in n for n in hot), "resident kernel remarks missing"
+    spilled = {n: r.get("ScratchSize") for n, r in hot.items() if r.get("ScratchSize", 0) != 0}
+    assert not spilled, f"scratch spills in hot kernels: {spilled}"
+    vspill = {n: r.get("VGPRs Spill") for n, r in hot.items() if r.get("VGPRs Spill", 0) != 0}
+    assert not vspill, f"VGPR spills in hot kernels: {vspill}"
+
+
+def test_resident_kernel_fits_three_waves_per_simd():
+    """The resident kernel's launch bound (768 threads = 3 waves per SIMD) caps it at
+    168 VGPRs; it must stay within that without spilling (checked above)."""
+    rows = _rows()
+    res = [r for n, r in rows.items() if "prop_resident_kernel" in n]
+    assert res and all(r["VGPRs"] <= 168 and r.get("Occupancy", 0) >= 3 for r in res), res
+
+
+@pytest.mark.parametrize("text,expect", [
+    ("x.h:1:1: remark: Function Name: _Zfoo [-R]\nx.h:1:1: remark:     VGPRs: 12 [-R]\n"
+     "x.h:1:1: remark:     ScratchSize [bytes/lane]: 8 [-R]\n", {"_Zfoo": {"VGPRs": 12, "ScratchSize": 8}}),
+])
+def test_parse(text, expect):
+    assert RU.parse(text) == expect
