@@ -566,6 +566,7 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
                       void *workspace, int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags) {
     if (!plan) return fail(NLSPN_EINVAL, "plan is null");
     *plan = nullptr;
+    (void)dev_state();  // its one-time host allocation must not happen inside the capture
     hipStream_t cs = nullptr;
     NLSPN_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);

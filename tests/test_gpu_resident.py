@@ -244,3 +244,20 @@ def test_aborted_launch_raises_and_poisons():
     torch.cuda.synchronize()
     _lib.check_resident()
     assert not torch.isnan(o["pred"]).any()
+
+
+def test_plan_first_in_fresh_process():
+    """A PropagationPlan created before any other library call (as bench.py does) in a
+    fresh process: the library's one-time per-device setup must not run inside the
+    plan's stream capture."""
+    import subprocess
+    import sys
+    code = ("import sys, torch; sys.path.insert(0, %r)\n"
+            "from nlspn_eccv20_amd import PropagationPlan\n"
+            "d = 'cuda:0'; B, H, W, K = 8, 228, 304, 8\n"
+            "x = lambda c: torch.rand((B, c, H, W), device=d)\n"
+            "oa = x(3 * K)\n"
+            "p = PropagationPlan(x(1), x(1), x(1), oa[:, 2 * K:], oa[:, :2 * K], torch.tensor([4.0], device=d))\n"
+            "p.replay(); p.check(); p.close(); print('ok')\n") % os.path.dirname(os.path.dirname(__file__))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
