@@ -83,6 +83,8 @@ def get() -> ctypes.CDLL:
                 "There is no CPU fallback for the propagation hot path.")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if not hasattr(lib, name) and os.environ.get("NLSPN_LIB_PATH") and name == "nlspn_resident_status":
+                continue  # A/B against an older build (ABI 2) without the status word
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -101,6 +103,8 @@ def check_resident(device=None) -> None:
     current one) aborted since the last check; clears the sticky word.  No device sync:
     an abort is seen once the aborted launch has finished."""
     lib = get()
+    if not hasattr(lib, "nlspn_resident_status"):
+        return
     if device is None:
         hit = lib.nlspn_resident_status(1)
     else:

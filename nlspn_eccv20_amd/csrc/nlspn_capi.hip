@@ -23,8 +23,12 @@
 
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
-extern template __global__ void prop_resident_kernel<float, kResMaxNT, 2>(ResArgs);
-extern template __global__ void prop_resident_kernel<__half, kResMaxNT, 2>(ResArgs);
+#define NLSPN_RES_EXTERN(T)                                                       \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 0>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 576>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 128>(ResArgs);
+NLSPN_RES_EXTERN(float)
+NLSPN_RES_EXTERN(__half)
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -193,14 +197,20 @@ int device_cus() {
 //    aborts (nlspn_resident.h); nlspn_resident_status reads it with no device sync.
 //  * res_guard: the resident kernel needs every workgroup co-resident, so two of
 //    its launches must never run at once on one device.  Resident launches are
-//    serialised across streams: a launch on a stream other than the previous
-//    resident launch's waits for that launch's event.  (Skipped while a stream is
-//    being captured: a plan re-applies the guard when it is launched.)
+//    serialised across streams.  While one stream issues them all (the common case)
+//    nothing is recorded: an event record per launch costs ~3 us of stream time
+//    (measured, C2).  The first resident launch on a second stream synchronises the
+//    device once (no handle of the earlier stream is touched: it may be gone) and
+//    switches the device to multi-stream mode, where every resident launch records
+//    an event and a launch on another stream waits for the previous one's event.
+//    (Skipped while a stream is being captured: a plan re-applies the guard when it
+//    is launched.)
 struct DevState {
     std::mutex m;
     unsigned *host_status = nullptr, *dev_status = nullptr;
     hipEvent_t last_ev = nullptr;
     hipStream_t last_stream = nullptr;
+    bool any = false, multi = false;
     bool init = false;
 };
 constexpr int kMaxDevices = 64;
@@ -233,23 +243,37 @@ bool stream_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
+bool res_guard_off() {  // A/B measurement only: NLSPN_RES_GUARD=0
+    static const bool off = [] { const char *e = getenv("NLSPN_RES_GUARD"); return e && e[0] == '0'; }();
+    return off;
+}
+
 int res_guard_before(hipStream_t s) {
-    if (stream_capturing(s)) return NLSPN_OK;
+    if (res_guard_off() || stream_capturing(s)) return NLSPN_OK;
     DevState *d = dev_state();
     if (!d) return NLSPN_OK;
     std::lock_guard<std::mutex> lk(d->m);
-    if (d->last_ev && d->last_stream != s) NLSPN_HIP_TRY(hipStreamWaitEvent(s, d->last_ev, 0));
+    if (d->any && d->last_stream != s) {
+        if (!d->multi) {  // first switch: everything earlier finishes, then record per launch
+            NLSPN_HIP_TRY(hipDeviceSynchronize());
+            d->multi = true;
+        } else if (d->last_ev) {
+            NLSPN_HIP_TRY(hipStreamWaitEvent(s, d->last_ev, 0));
+        }
+    }
     return NLSPN_OK;
 }
 
 int res_guard_after(hipStream_t s) {
-    if (stream_capturing(s)) return NLSPN_OK;
+    if (res_guard_off() || stream_capturing(s)) return NLSPN_OK;
     DevState *d = dev_state();
     if (!d) return NLSPN_OK;
     std::lock_guard<std::mutex> lk(d->m);
+    d->any = true;
+    d->last_stream = s;
+    if (!d->multi) return NLSPN_OK;
     if (!d->last_ev) NLSPN_HIP_TRY(hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
     NLSPN_HIP_TRY(hipEventRecord(d->last_ev, s));
-    d->last_stream = s;
     return NLSPN_OK;
 }
 
@@ -261,8 +285,10 @@ struct ResPlan {
 };
 
 template <typename T>
-const void *res_fn() {
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2>);
+const void *res_fn(long long nt) {
+    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 576>);
+    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 128>);
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 0>);
 }
 
 // Fills P and returns true when the resident kernel applies.
@@ -306,7 +332,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (lds > kLdsBytes || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
     const unsigned G = (unsigned)(B * g);
     if ((G + 1) * 4 > kSyncBytes) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>() : res_fn<__half>();
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(nt) : res_fn<__half>(nt);
     P.grid = G;
     P.block = (unsigned)nt;
     P.lds = lds;

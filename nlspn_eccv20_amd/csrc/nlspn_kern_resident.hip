@@ -5,6 +5,13 @@
 #include "nlspn_resident.h"
 
 namespace nlspn {
-template __global__ void prop_resident_kernel<float, kResMaxNT, 2>(ResArgs);
-template __global__ void prop_resident_kernel<__half, kResMaxNT, 2>(ResArgs);
+// NTC: compile-time thread counts of the shapes the bench configs plan (C2 NYU B=8:
+// 576; one NYU image, C1: 128), so the LDS row addresses fold into immediates;
+// 0 = any other shape (thread count read at run time).
+#define NLSPN_RES_INST(T)                                                  \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 0>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 576>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 128>(ResArgs);
+NLSPN_RES_INST(float)
+NLSPN_RES_INST(__half)
 }  // namespace nlspn

@@ -132,7 +132,8 @@ template <> struct ResVec<__half> {
 
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
 // MAXNT = launch bound (threads), SMAX = staging quads per thread per iteration.
-template <typename T, int MAXNT, int SMAX>
+// NTC = the thread count as a compile-time constant (0: blockDim.x at run time).
+template <typename T, int MAXNT, int SMAX, int NTC>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RX = kResRX;
     constexpr unsigned ES = sizeof(T);
@@ -143,9 +144,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (s[rx], s[rx+1]) is ONE 8-byte-aligned ds_read_b64 from one of the copies
     float *fwin = smem + 4;                                                      // [wh_max][WW]
     float *fwinB = fwin + (size_t)a.wh_max * WW;                                 // [wh_max][WW], shifted by 1
-    // [K+2][NT]: affinities, 1 - sum, and the own quad's conf' (1 with conf_prop off)
+    // [K+2][NT]: the K affinities, 1 - sum, and the own quad's conf' (1 with conf_prop
+    // off).  With a compile-time NT (NTC) every row is an immediate offset from one or
+    // two base registers (no per-row address registers to keep live across the loop).
     float4 *akl = reinterpret_cast<float4 *>(fwinB + (size_t)a.wh_max * WW);
-    const int NT = blockDim.x;
+    const int NT = NTC ? NTC : (int)blockDim.x;
     const int tid = threadIdx.x, lane = tid & 63;
 
     const int b = blockIdx.x % a.B, j = blockIdx.x / a.B;
@@ -316,7 +319,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     T *p_out_all = static_cast<T *>(a.pred_inter);
     const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
 
-    int t_abort = 0;
     for (int t = 1; t < a.T; ++t) {
         // The tap geometry depends only on the (invariant) coordinates, so the
         // compiler would hoist all 32 taps' weights and addresses out of this loop
@@ -329,10 +331,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
         asm volatile("" : "+v"(tb));
-        // and the thread's LDS affinity rows: without this the compiler keeps the ten
-        // row addresses live across the loop and spills them to scratch
-        int tq = tid;
-        asm volatile("" : "+v"(tq));
 
         unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                       ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
@@ -364,9 +362,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
         __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
-        if (ctl[0]) {  // aborted: poison what this part has not produced (below), then exit
-            t_abort = t;
-            break;
+        if (ctl[0]) {  // aborted: NaN in every plane this part has not written, then exit
+            if (active) {
+                const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+                for (int tt = t; tt < a.T; ++tt)
+                    ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * N + b * HW), vpix, 0u, qn);
+                ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, qn);
+            }
+            return;
         }
         if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
 
@@ -418,11 +421,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (k == REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
-                    const float4 ar = akl[K * NT + tq];
+                    const float4 ar = akl[K * NT + tid];
                     const float *c = &fwin[(y - rlo) * WW + x0 + RX];
                     acc[0] += c[0] * ar.x; acc[1] += c[1] * ar.y; acc[2] += c[2] * ar.z; acc[3] += c[3] * ar.w;
                 }
-                const float4 a4 = akl[k * NT + tq];
+                const float4 a4 = akl[k * NT + tid];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -448,11 +451,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll 1
                     for (int k = 0; k < K; ++k) {
                         if (k == REF) {
-                            const float4 ar = akl[K * NT + tq];
+                            const float4 ar = akl[K * NT + tid];
                             const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
                             s += fwin[(y - rlo) * WW + x0 + e + RX] * arv[e];
                         }
-                        const float4 a4 = akl[k * NT + tq];
+                        const float4 a4 = akl[k * NT + tid];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
                         const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
                         const float h_im = (float)(y - PH + i) +
@@ -519,7 +522,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
         // this iteration is done: the barrier above), as the next staging would load it
         if (t < a.T - 1 && active && !(a.dbg & 2u)) {
-            const float4 cw = akl[(K + 1) * NT + tq];
+            const float4 cw = akl[(K + 1) * NT + tid];
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
             if (has_conf) {
                 f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
@@ -530,12 +533,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
             fwinB[li + 2] = f.w;
         }
-    }
-    if (t_abort && active) {  // an aborted launch never looks valid: NaN in every unwritten plane
-        const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
-        for (int tt = t_abort; tt < a.T; ++tt)
-            ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * N + b * HW), vpix, 0u, qn);
-        ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, qn);
     }
 }
 

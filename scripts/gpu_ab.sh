@@ -1,12 +1,18 @@
 #!/bin/bash
-# Same-box A/B of two library builds (NLSPN_LIB_PATH): C2 bench value, alternated.
+# Same-box A/B of library builds / env toggles: C2 bench value, alternated rounds.
+# usage: scripts/gpu_ab.sh NAME=LIBPATH_OR_-[:ENV=VAL] ...   ("-" = the in-tree build)
+# e.g.   scripts/gpu_ab.sh cur=- r01=nlspn_eccv20_amd/lib/ab/libnlspn_r01.so noguard=-:NLSPN_RES_GUARD=0
 set -o pipefail
 O=gpurun_out/ab; mkdir -p $O
-B=nlspn_eccv20_amd/lib/ab/libnlspn_hip_head.so
+CFG=${AB_CONFIG:-nyu}
 for r in 1 2 3; do
-  for v in new head; do
-    if [ $v = head ]; then export NLSPN_LIB_PATH=$B; else unset NLSPN_LIB_PATH; fi
-    timeout -k 10 120 python bench.py --no-cpu-baseline --no-backward --no-gru --steps 200 --warmup 20 > $O/$v$r.json 2> $O/$v$r.err || exit 1
-    python -c "import json;d=json.load(open('$O/$v$r.json'));print('$v', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_mean'])"
+  for spec in "$@"; do
+    name=${spec%%=*}; rest=${spec#*=}; lib=${rest%%:*}; envs=""
+    [ "$rest" != "$lib" ] && envs=${rest#*:}
+    ( if [ "$lib" != "-" ]; then export NLSPN_LIB_PATH=$lib; else unset NLSPN_LIB_PATH; fi
+      for e in ${envs//,/ }; do export "$e"; done
+      timeout -k 10 120 python bench.py --config $CFG --no-cpu-baseline --no-backward --no-gru --no-extra-configs \
+          --steps 200 --warmup 20 > $O/$name$r.json 2> $O/$name$r.err ) || exit 1
+    python -c "import json;d=json.load(open('$O/$name$r.json'));print('$name', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_mean'])"
   done
 done
