@@ -24,7 +24,7 @@ HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # outside the LDS window) and once per iteration by the own-quad write-back.  Variants
 # forced to zero scratch measured 2-3 % slower (same-box A/B), so the cap
 # below only stops spills from growing.
-RESIDENT_SCRATCH_CAP = 32
+RESIDENT_SCRATCH_CAP = 40
 
 
 def _rows():
