@@ -23,13 +23,15 @@ runs its own batch shard (weak scaling, no collective on the data path; SURVEY
 §8e); the process group only carries the max-over-ranks timing and the per-rank
 spread.  `--dry-run` runs the launcher and sharding logic on CPU (gloo, no GPU).
 
-roofline (the dominant kernel: the resident kernel, iterations 2..T in one launch,
-where it applies, else the per-iteration step kernel):
+roofline (the dominant kernel: the resident kernel — iterations 2..T, one launch per
+image group (C2: one group of 8 images; C3: two of 2) — where it applies, else the
+per-iteration step kernel):
   achieved = COMPULSORY bytes per launch / its mean duration from dispatch-recorded
       HIP events (nlspn_time_propagate) on this stream.  Compulsory bytes are what
       the launch must move at least once: a step launch reads its 3K+3 input
-      planes and writes one (SURVEY §8(d)'s S*(4+3K) per pixel); the resident launch
-      reads the 3K+2 invariant planes and p_1 once and writes T-1 planes + pred.
+      planes and writes one (SURVEY §8(d)'s S*(4+3K) per pixel); the resident launches
+      read the 3K+2 invariant planes and p_1 once and write T-1 planes + pred (their
+      duration spans every group's launch).
       So frac <= 1 for any kernel that really moves its bytes.
   alg_8d   = the secondary figure on SURVEY §8(d)'s per-iteration basis
       (S*(4+3K) bytes per pixel-iteration x the pixel-iterations of one launch),
@@ -118,7 +120,7 @@ def make_inputs(cfg, rank, dev):
 def kernel_time(plan, inputs, cfg, reps, dev):
     """Dispatch-recorded HIP-event durations (nlspn_time_propagate) on this stream, over
     `reps` whole propagations on the plan's buffers: step 1 (prologue fused) and
-    iterations 2..T — one resident-kernel launch, or the sum of the T-1 step kernels."""
+    iterations 2..T — the resident-kernel launches (one per image group), or the sum of the T-1 step kernels."""
     from nlspn_eccv20_amd import _lib
     from nlspn_eccv20_amd.propagation import _ptr, _stream
     o = plan.outputs
@@ -131,7 +133,7 @@ def kernel_time(plan, inputs, cfg, reps, dev):
         _ptr(o["offset"]), _ptr(o["confidence"]), _ptr(o["workspace"]), cfg["B"], cfg["H"], cfg["W"],
         cfg["kernel"][0], cfg["kernel"][1], cfg["T"], _lib.AFF_KINDS["TGASS"], _lib.PRESERVE_INPUT, reps,
         _stream(dev), ctypes.byref(first), ctypes.byref(rest), ctypes.byref(res)))
-    return first.value, rest.value, bool(res.value)
+    return first.value, rest.value, int(res.value)
 
 
 def pmc_traffic(config, kernel):
@@ -163,7 +165,8 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
         # writes: pred_inter[1..T-1] and pred
         comp_planes = (K + 2 * K + 2 + 1) + (T - 1 + 1)
         alg_iters = T - 1
-        kdesc = f"{kname} (iterations 2..{T} in one launch, invariant planes on chip)"
+        kdesc = (f"{kname} (iterations 2..{T}, invariant planes on chip: {resident} launch(es), one per image "
+                 f"group; kernel_ms_mean spans them all)")
     else:
         kname, kmean = "prop_step_kernel", rest_ms / max(1, T - 1)
         comp_planes = 4 + 3 * K  # p_in, conf', dep, K aff, 2K offsets read; p_out written

@@ -24,9 +24,9 @@
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
 #define NLSPN_RES_EXTERN(T)                                                       \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 0>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 576>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 128>(ResArgs);
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128>(ResArgs);
 NLSPN_RES_EXTERN(float)
 NLSPN_RES_EXTERN(__half)
 }  // namespace nlspn
@@ -277,18 +277,66 @@ int res_guard_after(hipStream_t s) {
     return NLSPN_OK;
 }
 
+constexpr int kResMaxGroups = 64;  // image groups (back-to-back resident launches) per section
+
 struct ResPlan {
     const void *fn = nullptr;
-    unsigned grid = 0, block = 0;
+    unsigned block = 0;
     size_t lds = 0, sync_bytes = 0;
-    ResArgs a{};
+    int ngroups = 0;
+    unsigned grid[kResMaxGroups] = {};
+    ResArgs a[kResMaxGroups];
 };
 
 template <typename T>
 const void *res_fn(long long nt) {
-    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 576>);
-    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 128>);
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, 2, 0>);
+    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576>);
+    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128>);
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0>);
+}
+
+// The part grid of a resident launch: Bg images per launch, each cut into gy row
+// bands x gx quad-column bands (one workgroup per part, Bg*gy*gx <= CUs), nt threads
+// (one per quad of the largest part), win_cells LDS cells per window copy.
+struct ResShape {
+    int Bg = 0, gy = 0, gx = 0, nt = 0, win_cells = 0;
+};
+
+// The most images per launch (fewest launches) whose parts fit one workgroup and
+// whose fixed-halo window fits LDS; among the part grids of that image count, the
+// one with the least estimated work per iteration: the largest part's quads plus a
+// fifth per quad of its window rim restaged every iteration (a rim of ~9 px: the
+// 3x3 taps at N(0,2^2) offsets).  Measured weights: C2 taps 2.4 us for 542 quads,
+// staging 1.2 us for ~1350 quads.
+bool res_shape(int B, int H, int W, int cus, ResShape &S) {
+    const int W4 = W / 4;
+    const long long Q = (long long)H * W4;
+    for (int Bg = std::min(B, cus); Bg >= 1; --Bg) {
+        const int gmax = (int)std::min<long long>(cus / Bg, std::max<long long>(1, Q / 64));
+        double best = 1e300;
+        for (int g = gmax; g >= std::max(1, gmax * 3 / 4); --g) {
+            for (int gy = 1; gy <= g; ++gy) {
+                if (g % gy) continue;
+                const int gx = g / gy;
+                if (gy > H || gx > W4) continue;
+                const int ph = (H + gy - 1) / gy, pq = (W4 + gx - 1) / gx;
+                const int nq = ph * pq, nt = (nq + 63) / 64 * 64;
+                if (nt > kResMaxNT) continue;
+                const long long cells = res_win_cells(nt);
+                const long long fb = (long long)(ph + 2 * kResRY) * (4 * (pq + 2 * kResRXQ) + 2 * kResPadX);
+                if (cells < fb) continue;
+                const double R = 9.0;
+                const double rim = ((ph + 2 * R) * (4.0 * pq + 2 * R) - 4.0 * nq) / 4.0;
+                const double cost = nq + 0.2 * rim;
+                if (cost < best) {
+                    best = cost;
+                    S.Bg = Bg; S.gy = gy; S.gx = gx; S.nt = nt; S.win_cells = (int)cells;
+                }
+            }
+        }
+        if (best < 1e300) return true;
+    }
+    return false;
 }
 
 // Fills P and returns true when the resident kernel applies.
@@ -303,61 +351,72 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
         return false;
     const int cus = device_cus();
-    if (cus < 1 || B > cus) return false;
-    const long long W4 = W / 4, Q = (long long)H * W4;
+    if (cus < 1) return false;
     const long long HW = (long long)H * W;
     if (HW * 9 * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into a 9-plane item
-    // the most parts per image (up to one workgroup per CU) whose quads fit one
-    // workgroup; LDS: the f window (as many rows as fit, at least the part's rows
-    // + 2 RY) and the per-thread affinity rows
-    constexpr size_t kLdsBytes = 160 * 1024;
-    const long long WWb = 4LL * (W + 2 * kResRX);
-    int g = (int)std::min<long long>(cus / B, Q / 64);
-    long long nt = 0, wh_max = 0;
-    for (; g >= 1; --g) {
-        long long qmax = 0, rows_max = 0;
-        for (int j = 0; j < g; ++j) {
-            const long long qlo = (long long)j * Q / g, qhi = (long long)(j + 1) * Q / g;
-            qmax = std::max(qmax, qhi - qlo);
-            rows_max = std::max(rows_max, (qhi - 1) / W4 - qlo / W4 + 1);
+    ResShape S;
+    if (!res_shape(B, H, W, cus, S)) return false;
+    if (const char *gs = getenv("NLSPN_RES_GRID")) {  // A/B only: "gy,gx" part grid (same images per launch)
+        int gy = 0, gx = 0;
+        if (sscanf(gs, "%d,%d", &gy, &gx) == 2 && gy >= 1 && gx >= 1 && gy <= H && gx <= W / 4 &&
+            S.Bg * gy * gx <= cus) {
+            const int ph = (H + gy - 1) / gy, pq = (W / 4 + gx - 1) / gx, nt = (ph * pq + 63) / 64 * 64;
+            if (nt <= kResMaxNT &&
+                (long long)(ph + 2 * kResRY) * (4 * (pq + 2 * kResRXQ) + 2 * kResPadX) <= res_win_cells(nt)) {
+                S.gy = gy; S.gx = gx; S.nt = nt; S.win_cells = res_win_cells(nt);
+            }
         }
-        nt = (qmax + 63) / 64 * 64;
-        if (nt > kResMaxNT) break;  // fewer parts only makes them larger
-        const long long avail = (long long)kLdsBytes - 16 - 16LL * 10 * nt;
-        wh_max = avail > 0 ? avail / (2 * WWb) : 0;  // two copies of the window
-        if (wh_max >= rows_max + 2 * kResRY) break;
     }
-    if (g < 1 || nt > kResMaxNT || wh_max < 1) return false;
-    const size_t lds = 16 + (size_t)(2 * wh_max * WWb) + 16 * 10 * (size_t)nt;
-    if (lds > kLdsBytes || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
-    const unsigned G = (unsigned)(B * g);
+    const int ng = (B + S.Bg - 1) / S.Bg;
+    if (ng > kResMaxGroups) return false;
+    const unsigned G = (unsigned)(S.Bg * S.gy * S.gx);
     if ((G + 1) * 4 > kSyncBytes) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(nt) : res_fn<__half>(nt);
-    P.grid = G;
-    P.block = (unsigned)nt;
+    const size_t lds = 4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt;
+    if (lds > (size_t)kResLds || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt) : res_fn<__half>(S.nt);
+    P.block = (unsigned)S.nt;
     P.lds = lds;
     P.sync_bytes = ((G + 1) * 4 + 15) / 16 * 16;
+    P.ngroups = ng;
     DevState *ds = dev_state();
-    P.a = ResArgs{conf_eff, (flags & kPreserve) ? dep : nullptr, aff_norm, off_raw, pred_inter, pred,
-                  static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, B, H, W, T, g,
-                  (int)wh_max, flags, 0u};
-    if (const char *d = getenv("NLSPN_RES_DBG")) P.a.dbg = (unsigned)atoi(d);
+    unsigned dbg = 0;
+    if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
+    const int K = 8;
+    for (int k = 0; k < ng; ++k) {
+        const long long b0 = (long long)k * S.Bg;
+        const int Bk = (int)std::min<long long>(S.Bg, B - b0);
+        auto at = [&](const void *p, long long elems) -> const void * {
+            return p ? static_cast<const char *>(p) + (size_t)(elems * (long long)es) : nullptr;
+        };
+        P.grid[k] = (unsigned)(Bk * S.gy * S.gx);
+        P.a[k] = ResArgs{at(conf_eff, b0 * HW), (flags & kPreserve) ? at(dep, b0 * HW) : nullptr,
+                         at(aff_norm, b0 * (K + 1) * HW), at(off_raw, b0 * off_bs),
+                         const_cast<void *>(at(pred_inter, b0 * HW)), const_cast<void *>(at(pred, b0 * HW)),
+                         static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
+                         Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * T), flags, dbg};
+    }
     return true;
 }
 
 // The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words).
+// e0 is recorded at the start of the first group's launch, e1 at the end of the last.
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
-    if (g_rec) g_rec->push_back(LaunchRec{P.fn, dim3(P.grid), dim3(P.block), P.lds, true, StepArgs{}, P.a});
-    int rc = res_guard_before(s);
-    if (rc) return rc;
-    void *args[] = {&P.a};
-    if (e0)
-        NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s, e0, e1, 0));
-    else
-        NLSPN_HIP_TRY(hipLaunchKernel(P.fn, dim3(P.grid), dim3(P.block), args, P.lds, s));
-    if ((rc = check_launch("nlspn_propagate resident"))) return rc;
-    return res_guard_after(s);
+    for (int k = 0; k < P.ngroups; ++k) {
+        if (g_rec)
+            g_rec->push_back(LaunchRec{P.fn, dim3(P.grid[k]), dim3(P.block), P.lds, true, StepArgs{}, P.a[k]});
+        int rc = res_guard_before(s);
+        if (rc) return rc;
+        void *args[] = {&P.a[k]};
+        hipEvent_t s0 = k == 0 ? e0 : nullptr, s1 = k == P.ngroups - 1 ? e1 : nullptr;
+        if (s0 || s1)
+            NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s, s0, s1, 0));
+        else
+            NLSPN_HIP_TRY(hipLaunchKernel(P.fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s));
+        if ((rc = check_launch("nlspn_propagate resident"))) return rc;
+        if ((rc = res_guard_after(s))) return rc;
+    }
+    return NLSPN_OK;
 }
 
 // ------------------------------------------------------- affinity-normalisation dispatch
@@ -480,12 +539,12 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
                                    pred, workspace, B, H, W, kh, kw, T, flags, P);
     if (res) {  // step 1 zeroes the resident kernel's progress words
-        r1.a.zero_words = P.a.sync;
+        r1.a.zero_words = P.a[0].sync;
         r1.a.nzero = (int)(P.sync_bytes / 4);
     }
     if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
     if (res) {
-        if (resident) *resident = 1;
+        if (resident) *resident = P.ngroups;
         return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
     }
     for (int t = 1; t < T; ++t) {  // list_pred[t] lands in pred_inter[t]
@@ -571,13 +630,11 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
                           as_stream(stream), nullptr, nullptr);
 }
 
-// A plan replays the captured section as one hipGraph, except when it is at most
-// kPlanDirectMax launches (the resident path: step 1 + one resident launch): there
-// a graph launch costs more than the launches it saves (C2: 152.5 vs 147.3 us per
-// step, tools/launch_probe.py), so the recorded launches are re-issued directly.
+// A plan replays the captured section as one hipGraph, except on the resident path
+// (step 1 + one resident launch per image group): there a graph launch costs more
+// than the launches it saves (C2: 152.5 vs 147.3 us per step,
+// tools/launch_probe.py), so the recorded launches are re-issued directly.
 // NLSPN_PLAN_GRAPH=1 forces the graph.
-constexpr size_t kPlanDirectMax = 2;
-
 struct nlspn_plan {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -624,8 +681,8 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
     p->graph = g;
     p->exec = ge;
     const char *env = getenv("NLSPN_PLAN_GRAPH");
-    p->direct = recs.size() <= kPlanDirectMax && !(env && env[0] == '1');
     for (const LaunchRec &r : recs) p->resident = p->resident || r.resident;
+    p->direct = (p->resident || recs.size() <= 2) && !(env && env[0] == '1');
     p->recs = std::move(recs);
     *plan = p;
     return NLSPN_OK;
@@ -1034,7 +1091,7 @@ int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T,
     if (!plan_resident(dtype, has_conf ? d : nullptr, d, d, d, 2LL * (kh * kw - 1) * H * W, d, d, d, B, H, W, kh,
                        kw, T, NLSPN_PRESERVE_INPUT, P))
         return 0;
-    if (grid) *grid = (int)P.grid;
+    if (grid) *grid = (int)P.grid[0];
     if (block) *block = (int)P.block;
     if (lds_bytes) *lds_bytes = (int)P.lds;
     return 1;

@@ -9,9 +9,9 @@ namespace nlspn {
 // 576; one NYU image, C1: 128), so the LDS row addresses fold into immediates;
 // 0 = any other shape (thread count read at run time).
 #define NLSPN_RES_INST(T)                                                  \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 0>(ResArgs);   \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 576>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, 2, 128>(ResArgs);
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128>(ResArgs);
 NLSPN_RES_INST(float)
 NLSPN_RES_INST(__half)
 }  // namespace nlspn

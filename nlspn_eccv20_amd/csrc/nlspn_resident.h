@@ -1,45 +1,51 @@
-// Resident propagation: iterations 2..T of the NLSPN loop in ONE launch, with
-// every iteration-invariant plane held on chip.
+// Resident propagation: iterations 2..T of the NLSPN loop in ONE launch per image
+// group, with every iteration-invariant plane held on chip.
 //
 // Why: a per-iteration launch (nlspn_step.h) must re-read the invariant planes
 // — K normalised affinities, 2K offsets, conf', dep: 27 fp32 planes = 108 of its
 // 112 B/px at K=8 — every iteration, so it is HBM-bound at ~6 TB/s however it is
 // tiled.  Those planes do not change between iterations (nlspnmodel.py:340-363
-// re-uses offset / aff / confidence / dep), and at NYU size (C2: 60 MB) they fit
-// in the register files (128 MB chip-wide).  So this kernel keeps them there:
+// re-uses offset / aff / confidence / dep), and a group of images whose planes fit
+// the register files and LDS (C2: all 8 NYU images, 60 MB; C3: 2 of the 4 KITTI
+// images) keeps them there:
 //
-//   * one workgroup per CU owns a contiguous run of pixel quads of ONE image
-//     (image b = blockIdx % B, part j = blockIdx / B, so an image's parts share
-//     an XCD group); each thread owns one quad (4 pixels of a row) and holds its
-//     26 invariant words per pixel (8 affinities, the reference-tap weight
-//     1 - sum, 16 offsets, dep) in VGPRs for the whole launch;
-//   * the part's conf' window (its rows +- RY, the full width +- RX, zero
-//     outside the image) lives in LDS for the whole launch;
-//   * per iteration only the previous depth plane moves: the window rows of
-//     p_{t-1} are loaded (write-through hand-off, below), multiplied by conf'
-//     into the LDS f-window, the taps are sampled exactly as prop_step_kernel
-//     does (same IEEE sequence: bit-identical), and p_t is stored.
+//   * one workgroup per CU owns a RECTANGLE of pixel quads of one image (image
+//     b = blockIdx % B, part j = blockIdx / B = py * gx + px of a gy x gx grid of
+//     row bands x quad-column bands, so an image's parts share an XCD group); each
+//     thread owns one quad (4 pixels of a row) and holds its tap geometry and dep
+//     in VGPRs, its affinities and conf' in LDS, for the whole launch;
+//   * the part's f window — every cell any valid tap of the part reads (found once:
+//     offsets are invariant), zero outside the image — lives in LDS;
+//   * per iteration only the previous depth plane moves: the window cells of
+//     p_{t-1} owned by OTHER parts are loaded (write-through hand-off, below),
+//     multiplied by conf' into the window, the taps are sampled exactly as
+//     prop_step_kernel does (same IEEE sequence: bit-identical), and p_t is stored.
+//     Rectangular parts keep that staging to the window's rim: at C2 about a
+//     third of the cells a full-width row band would restage.
 //
 // Between iterations a part waits only for the parts its window (and any
-// out-of-window tap) reads — a contiguous range of parts of its own image,
-// computed once from the invariant offsets — through per-workgroup progress
-// words.  Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, the
-// write-through row of MI355X_MICROARCH.md § inter-workgroup visibility):
+// out-of-window tap) reads — a rectangle of parts of its own image, computed once
+// from the invariant offsets — through per-workgroup progress words.  Hand-off
+// protocol (cdna_hip_programming.md §6 Guideline 16, the write-through row of
+// MI355X_MICROARCH.md § inter-workgroup visibility):
 //   producer: every p_t store is `sc1` (write-through), every wave drains
 //             (s_waitcnt vmcnt(0)), workgroup barrier, ONE lane stores its
-//             progress word = t (relaxed, agent scope = sc1 store);
+//             progress word = epoch + t (relaxed, agent scope = sc1 store);
 //   consumer: ONE wave polls the words it depends on (relaxed sc1 loads),
 //             workgroup barrier, then EVERY load of a pred_inter plane is an
 //             `sc1` load (no acquire fence needed, L1 bypassed).
 // Loads of bytes not written in this launch (conf', invariants) are plain.
 // Every plane t is written once, so there is no write-after-read hazard and a
-// fast part may run ahead of parts that do not feed it.
+// fast part may run ahead of parts that do not feed it.  Image groups run as
+// back-to-back launches on one stream; group k's progress values start at
+// epoch = k * T, above everything group k-1 left in the words, so the words are
+// zeroed once per section (by step 1).
 //
-// Residency: G = B * g workgroups (g parts per image), at most one per CU (the
-// dynamic LDS request exceeds half a CU's LDS) and G <= CU count, so the whole
-// grid is resident (the host serialises resident launches of one device across
-// streams, nlspn_capi.hip res_guard).  Every spin is bounded: on timeout a part
-// raises the abort word (sync[G]) and the device's host-mapped sticky status word
+// Residency: G = B * gy * gx workgroups, at most one per CU (the dynamic LDS
+// request exceeds half a CU's LDS) and G <= CU count, so the whole grid is
+// resident (the host serialises resident launches of one device across streams,
+// nlspn_capi.hip res_guard).  Every spin is bounded: on timeout a part raises the
+// abort word (sync[0]) and the device's host-mapped sticky status word
 // (ResArgs::status, read by nlspn_resident_status without a device sync), and every
 // part that sees the abort fills its own quads of the planes it has not written
 // (and pred) with NaN before it exits: an aborted launch never looks valid.
@@ -53,18 +59,20 @@ namespace nlspn {
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 struct ResArgs {
-    const void *conf;   // conf' (B planes) or null (conf_prop off)
-    const void *dep;    // B planes or null (preserve off)
+    const void *conf;   // conf' of this launch's images (planes H*W apart), or null (conf_prop off)
+    const void *dep;    // planes H*W apart, or null (preserve off)
     const void *aff;    // normalised affinity, (K+1) planes per item, contiguous (aff_out)
     const void *off;    // raw offsets, 2K planes per item, batch stride off_bs
-    void *pred_inter;   // T x B planes: iteration t reads plane t-1, writes plane t
-    void *pred;         // B planes: max(p_T, 0) (nlspnmodel.py:375-377)
-    unsigned *sync;     // [G] progress words, [G] abort word; zeroed before every launch
+    void *pred_inter;   // plane (t, b) at t * tstride + b * H * W: iteration t reads t-1, writes t
+    void *pred;         // planes H*W apart: max(p_T, 0) (nlspnmodel.py:375-377)
+    unsigned *sync;     // [0] abort word, [1 + blockIdx] progress words; zeroed by step 1
     unsigned *status;   // host-mapped sticky abort flag of the device (nlspn_resident_status), or null
     long long off_bs;   // elements
-    int B, H, W, T;
-    int g;              // parts (workgroups) per image
-    int wh_max;         // LDS window rows allocated per buffer
+    long long tstride;  // elements between iteration planes (B_section * H * W)
+    int B, H, W, T;     // B: images of this launch
+    int gy, gx;         // parts per image: gy row bands x gx quad-column bands
+    int win_cells;      // LDS cells per copy of the f window: res_win_cells(blockDim.x)
+    unsigned epoch;     // progress-word base of this launch (k * T for image group k)
     unsigned flags;
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
                         // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid),
@@ -72,7 +80,23 @@ struct ResArgs {
 };
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
-constexpr int kResRY = 8, kResRX = 8;            // window halo (rows, columns)
+#ifndef NLSPN_RES_SMAX
+#define NLSPN_RES_SMAX 1
+#endif
+constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per round
+constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, quad columns
+constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
+constexpr int kResCtl = 8;                       // LDS control words ahead of the window
+constexpr int kResAS = 11;                       // float4 per thread: K = 8 affinities, 1 - sum, conf', dep
+constexpr int kResLds = 160 * 1024;              // LDS per CU
+
+// LDS cells per copy of the f window for nt threads: what the per-thread rows leave,
+// a multiple of 4 (16-B aligned copies), both copies addressable by 16-bit indices.
+__host__ __device__ constexpr int res_win_cells(int nt) {
+    return ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4) < 32764
+               ? ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4)
+               : 32764;
+}
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
 #ifndef NLSPN_RES_NOGP
 constexpr bool kResGeneralPath = true;
@@ -81,10 +105,34 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 #endif
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 
-// Part j of an image with Q quads owns quads [j*Q/g, (j+1)*Q/g); owner(q) is the
-// largest j with floor(j*Q/g) <= q.
-__device__ __forceinline__ int res_owner(long long q, long long Q, int g) {
-    return (int)(((q + 1) * g - 1) / Q);
+// Band i of n over a length L owns [i*L/n, (i+1)*L/n); owner(v) is the largest i
+// with floor(i*L/n) <= v.
+__device__ __forceinline__ int res_owner(int v, int L, int n) { return (int)(((long long)(v + 1) * n - 1) / L); }
+
+// q = k / d for 0 <= k < 2^22, d >= 1, by the float reciprocal rd = 1/d plus one
+// correction step (the product is within 1 of the quotient at these sizes).
+__device__ __forceinline__ int res_div(int k, int d, float rd) {
+    int q = (int)((float)k * rd);
+    const int r = k - q * d;
+    q += r < 0 ? -1 : (r >= d ? 1 : 0);
+    return q;
+}
+
+// Merges lane spans (rows mn..mx, columns cmn..cmx) of the lanes with `on` into
+// ctl[1..4]: a wave reduction first, then one LDS atomic per wave and bound (576
+// lanes' atomics on 4 words serialise: 4.7 us of the setup at C2).
+__device__ __forceinline__ void res_span_merge(int *ctl, bool on, int mn, int mx, int cmn, int cmx) {
+    if (!on) { mn = cmn = 0x7fffffff; mx = cmx = -0x7fffffff; }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        mn = min(mn, __shfl_xor(mn, d));
+        mx = max(mx, __shfl_xor(mx, d));
+        cmn = min(cmn, __shfl_xor(cmn, d));
+        cmx = max(cmx, __shfl_xor(cmx, d));
+    }
+    if ((threadIdx.x & 63) == 0 && mn <= mx) {
+        atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); atomicMin(&ctl[3], cmn); atomicMax(&ctl[4], cmx);
+    }
 }
 
 // A value as storage type T holds it (fp32: itself; fp16: rounded), back in fp32.
@@ -131,52 +179,62 @@ template <> struct ResVec<__half> {
 };
 
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
-// MAXNT = launch bound (threads), SMAX = staging quads per thread per iteration.
+// MAXNT = launch bound (threads), SMAX = staging quads per thread per round.
 // NTC = the thread count as a compile-time constant (0: blockDim.x at run time).
 template <typename T, int MAXNT, int SMAX, int NTC>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
-    constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RX = kResRX;
+    constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RXQ = kResRXQ, PADX = kResPadX;
     constexpr unsigned ES = sizeof(T);
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    int *ctl = reinterpret_cast<int *>(smem);  // [0] abort, [1] / [2] row range scratch
-    const int H = a.H, W = a.W, WW = W + 2 * RX, W4 = W / 4;
+    // [0] abort, [1] / [2] row range, [3] / [4] column range (scratch of the setup)
+    int *ctl = reinterpret_cast<int *>(smem);
     // f window twice: fwin[i] and fwinB[i] = fwin[i + 1], so any horizontal pair
     // (s[rx], s[rx+1]) is ONE 8-byte-aligned ds_read_b64 from one of the copies
-    float *fwin = smem + 4;                                                      // [wh_max][WW]
-    float *fwinB = fwin + (size_t)a.wh_max * WW;                                 // [wh_max][WW], shifted by 1
-    // [K+2][NT]: the K affinities, 1 - sum, and the own quad's conf' (1 with conf_prop
-    // off).  With a compile-time NT (NTC) every row is an immediate offset from one or
-    // two base registers (no per-row address registers to keep live across the loop).
-    float4 *akl = reinterpret_cast<float4 *>(fwinB + (size_t)a.wh_max * WW);
+    // With a compile-time thread count the window size is one too (res_win_cells),
+    // so every fwinB access is an immediate offset from its fwin address.
     const int NT = NTC ? NTC : (int)blockDim.x;
+    const int WC = NTC ? res_win_cells(NTC) : a.win_cells;
     const int tid = threadIdx.x, lane = tid & 63;
+    float *fwin = smem + kResCtl;                                            // [WH][WW] used of WC
+    float *fwinB = fwin + WC;                                                // shifted by 1
+    // Per thread, kResAS float4 (thread-major, an odd count of 16-B rows: conflict-
+    // free ds_read_b128 across lanes): the K affinities, 1 - sum, the own quad's conf'
+    // (1 with conf_prop off) and dep (0 with preserve off) — every one an immediate
+    // offset from ONE address register.
+    float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
 
+    const int H = a.H, W = a.W, W4 = W / 4;
     const int b = blockIdx.x % a.B, j = blockIdx.x / a.B;
-    const long long Q = (long long)H * W4;
-    const long long qlo = (long long)j * Q / a.g, qhi = (long long)(j + 1) * Q / a.g;
-    const int prow0 = (int)(qlo / W4), prow1 = (int)((qhi - 1) / W4);  // the part's own rows
+    const int py = j / a.gx, px = j % a.gx;
+    const int r0 = (int)((long long)py * H / a.gy), r1 = (int)((long long)(py + 1) * H / a.gy);    // own rows
+    const int c0 = (int)((long long)px * W4 / a.gx), c1 = (int)((long long)(px + 1) * W4 / a.gx);  // own quad cols
+    const int nqw = c1 - c0, nown = (r1 - r0) * nqw;
 
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
-    const long long HW = (long long)H * W, N = (long long)a.B * HW;
+    const long long HW = (long long)H * W;
     const unsigned plane_bytes = (unsigned)HW * ES;
     gu32 *sync = (gu32 *)(a.sync);
-    const int G = gridDim.x;
 
-    // ---- own quad and its invariants (registers for the whole launch).  Taps are
-    // held as their sample coordinates (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw),
-    // the reference's own expression (.cuh:178-179), so an iteration starts from them.
+    // ---- own quad and its invariants.  Taps are held as their sample coordinates
+    // (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw), the reference's own
+    // expression (.cuh:178-179), so the geometry below starts from them.
     // trace (dbg 8): row t = 0 of this part holds the setup stamps
     unsigned long long *trace0 = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                    (size_t)blockIdx.x * a.T * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
-    const long long q = qlo + tid;
-    const bool active = q < qhi;
-    const int y = active ? (int)(q / W4) : 0, x0 = active ? (int)(q % W4) * 4 : 0;
+    const bool active = tid < nown;
+    int y = r0, x0 = 4 * c0;
+    if (active) {
+        const int rr = tid / nqw;
+        y = r0 + rr;
+        x0 = 4 * (c0 + tid - rr * nqw);
+    }
     const unsigned vpix = (unsigned)(y * W + x0) * ES;
-    float hy[K][4], hx[K][4], dv[4];
+    float hy[K][4], hx[K][4];
     {
+        float dv[4];
         float ak[K][4], aref[4];
         const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
@@ -199,22 +257,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
 #pragma unroll
-        for (int k = 0; k < K; ++k) akl[k * NT + tid] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
-        akl[K * NT + tid] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+        for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
+        akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
         float cq[4] = {1.f, 1.f, 1.f, 1.f};
         if (has_conf) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), vpix, 0u, cq);
-        akl[(K + 1) * NT + tid] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+        akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+        akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
     }
 
-    // ---- the window: every row a valid tap of this part touches (offsets are
-    // invariant, so once), when that span fits the LDS rows allocated; otherwise
-    // the part's rows +- RY, and the rare taps outside it take the general path.
-    if (tid == 0) { ctl[0] = 0; ctl[1] = prow0; ctl[2] = prow1; }  // own rows: the reference tap
+    // ---- the window: the rectangle of every cell a valid tap of this part touches
+    // (offsets are invariant, so once), when it fits the LDS cells allocated;
+    // otherwise the part +- (RY rows, RXQ quads), and the rare taps outside it take
+    // the general path.  Columns are whole quads plus PADX zero columns each side.
+    if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1 - 1; ctl[3] = 4 * c0; ctl[4] = 4 * c1 - 1; }
     __syncthreads();
     if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
     const float Hf = (float)H, Wf = (float)W;
     {
-        int mn = prow0, mx = prow1;
+        int mn = r0, mx = r1 - 1, cmn = 4 * c0, cmx = 4 * c1 - 1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
@@ -225,40 +285,45 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 hy[k][e] = h_im;
                 hx[k][e] = w_im;
                 if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                    const int h_low = (int)floorf(h_im);
+                    const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
                     mn = min(mn, h_low);
                     mx = max(mx, h_low + 1);
+                    cmn = min(cmn, w_low);
+                    cmx = max(cmx, w_low + 1);
                 }
             }
         }
-        if (active) { atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); }
+        res_span_merge(ctl, active, mn, mx, cmn, cmx);
     }
     __syncthreads();
-    int rlo = ctl[1], rhi = ctl[2];
-    if (rhi - rlo + 1 > a.wh_max) {  // span too tall for LDS: fixed halo + general path
-        rlo = prow0 - RY;
-        rhi = rlo + a.wh_max - 1;
+    int rlo = ctl[1], rhi = ctl[2], wq0 = ctl[3] >> 2, wq1 = ctl[4] >> 2;  // >> 2: floor for negatives too
+    if (rhi < rlo + 1) rhi = rlo + 1;  // at least two rows (the zero redirect reads a 2x2 footprint)
+    if ((rhi - rlo + 1) * (4 * (wq1 - wq0 + 1) + 2 * PADX) > WC) {  // too large: fixed halo + general path
+        rlo = r0 - RY;
+        rhi = r1 - 1 + RY;
+        wq0 = c0 - RXQ;
+        wq1 = c1 - 1 + RXQ;
     }
-    const int WH = rhi - rlo + 1;
-    const int ra = rlo < 0 ? 0 : rlo, rb = rhi > H - 1 ? H - 1 : rhi;  // in-image window rows
-    const int nsq = (rb - ra + 1) * W4;                                // staging quads per iteration
-    const int iown0 = (int)(qlo - (long long)ra * W4), iown1 = (int)(qhi - (long long)ra * W4);  // own ones
+    const int WH = rhi - rlo + 1, WWp = 4 * (wq1 - wq0 + 1), WW = WWp + 2 * PADX;
+    const int ra = max(rlo, 0), rb = min(rhi, H - 1);      // in-image window rows
+    const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
+    const int wqn = qb - qa + 1;
     __syncthreads();
-    if (tid == 0) { ctl[1] = ra; ctl[2] = rb; }
+    if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     __syncthreads();
     if (trace0 && tid == 0) trace0[2] = __builtin_amdgcn_s_memrealtime();
     // Classify every tap once:
     //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
-    //    coordinates are redirected to (rlo, -RX), an integer point of the window's
-    //    zero padding columns, so the branch-free path reads four zeros with weights
-    //    (1,0,0,0): v = +0 exactly, as the reference's val = 0;
+    //    coordinates are redirected to (rlo, 4*wq0 - PADX), an integer point of the
+    //    window's zero padding columns, so the branch-free path reads four zeros with
+    //    weights (1,0,0,0): v = +0 exactly, as the reference's val = 0;
     //  * in the LDS window: the branch-free path;
-    //  * valid but outside the window (only with a too-tall span): read from global
-    //    memory by the general path (has_fb); the dependency rows cover it.
+    //  * valid but outside the window (only with the fixed halo): read from global
+    //    memory by the general path (has_fb); the dependency rectangle covers it.
     bool has_fb = false;
     {
-        int mn = H, mx = -1;
+        int mn = H, mx = -1, cmn = W, cmx = -1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
@@ -266,25 +331,29 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float h_im = hy[k][e], w_im = hx[k][e];
                 if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                     const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
-                    const int ry = h_low - rlo, rx = w_low + RX;
-                    if (!((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1))) {
+                    if (!((unsigned)(h_low - rlo) < (unsigned)(WH - 1) &&
+                          (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1))) {
                         has_fb = true;
                         mn = min(mn, max(h_low, 0));
                         mx = max(mx, min(h_low + 1, H - 1));
+                        cmn = min(cmn, max(w_low, 0));
+                        cmx = max(cmx, min(w_low + 1, W - 1));
                     }
                 } else {
                     hy[k][e] = (float)rlo;
-                    hx[k][e] = -(float)RX;
+                    hx[k][e] = (float)(4 * wq0 - PADX);
                 }
             }
         }
         has_fb = has_fb && active;
-        if (has_fb) { atomicMin(&ctl[1], mn); atomicMax(&ctl[2], mx); }
+        res_span_merge(ctl, has_fb, mn, mx, cmn, cmx);
     }
     __syncthreads();
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
-    const int jlo = res_owner((long long)ctl[1] * W4, Q, a.g);
-    const int jhi = res_owner((long long)(ctl[2] + 1) * W4 - 1, Q, a.g);
+    // the parts this one reads: a rectangle of the image's part grid
+    const int dy0 = res_owner(ctl[1], H, a.gy), dy1 = res_owner(ctl[2], H, a.gy);
+    const int dx0 = res_owner(ctl[3] >> 2, W4, a.gx), dx1 = res_owner(ctl[4] >> 2, W4, a.gx);
+    const int ndx = dx1 - dx0 + 1, ndep = (dy1 - dy0 + 1) * ndx;
     const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
     // Every tap's bilinear geometry is iteration-invariant, so it is resolved once:
     // the fractional parts lh = h - floor(h), lw = w - floor(w) (.cuh:35-36, the same
@@ -296,7 +365,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     unsigned adp[K][2];
     {
         const float WWf = (float)WW;
-        const int lbase = RX - rlo * WW, bofs = a.wh_max * WW - 1;
+        const int lbase = PADX - 4 * wq0 - rlo * WW, bofs = WC - 1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             adp[k][0] = adp[k][1] = 0u;
@@ -305,8 +374,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float fh = floorf(hy[k][e]), fw = floorf(hx[k][e]);
                 lhv[k][e] = hy[k][e] - fh;
                 lwv[k][e] = hx[k][e] - fw;
-                // window index (h_low - rlo) * WW + w_low + RX, in exact float arithmetic;
-                // out-of-window (general-path) taps are clamped to cell 0 and never read
+                // window index (h_low - rlo) * WW + w_low - 4 wq0 + PADX, in exact float
+                // arithmetic; out-of-window (general-path) taps are clamped to cell 0 and
+                // never read
                 int li = (int)(fh * WWf + fw) + lbase;
                 li = ((unsigned)li < (unsigned)(WH * WW)) ? li : 0;
                 const unsigned idx = (li & 1) ? (unsigned)(li + bofs) : (unsigned)li;
@@ -315,9 +385,18 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
     }
 
+    // Staging map (iterations t >= 2): the in-image window quads outside the own
+    // rectangle — the bands above and below it (full window width), then the
+    // columns left and right of it.  Iteration 1 stages the whole in-image window.
+    const int ntop = r0 - ra, nband = (ntop + rb - r1 + 1) * wqn;
+    const int side = wqn - nqw, left = c0 - qa;
+    const int nall = (rb - ra + 1) * wqn, nrest = nall - nown;
+    const float rwqn = 1.0f / (float)wqn, rside = 1.0f / (float)(side > 0 ? side : 1);
+
     const T *p_all = static_cast<const T *>(a.pred_inter);
     T *p_out_all = static_cast<T *>(a.pred_inter);
     const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
+    const int lown = (y - rlo) * WW + x0 - 4 * wq0 + PADX;  // window cell of the own quad's first pixel
 
     for (int t = 1; t < a.T; ++t) {
         // The tap geometry depends only on the (invariant) coordinates, so the
@@ -339,16 +418,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
             bool fail = (a.dbg & 32u) && blockIdx.x == 0;  // test hook: part 0 of image 0 aborts
-            for (int base = jlo; base <= jhi && !fail; base += 64) {
-                const int jj = base + lane;
+            const unsigned need = a.epoch + (unsigned)(t - 1);
+            for (int base = 0; base < ndep && !fail; base += 64) {
+                const int d = base + lane;
+                const int dy = d / ndx;
+                const int jj = (dy0 + dy) * a.gx + dx0 + (d - dy * ndx);
                 for (;;) {
                     bool ok = true;
-                    if (jj <= jhi)
-                        ok = __hip_atomic_load(&sync[jj * a.B + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                             (unsigned)(t - 1);
+                    if (d < ndep)
+                        ok = __hip_atomic_load(&sync[1 + jj * a.B + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                             need;
                     if (__all(ok)) break;
                     if (++spins > kResSpinLimit ||
-                        __hip_atomic_load(&sync[G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                        __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
                         fail = true;
                         break;
                     }
@@ -357,7 +439,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
             if (fail && lane == 0) {
                 ctl[0] = 1;
-                __hip_atomic_store(&sync[G], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
@@ -366,7 +448,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (active) {
                 const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
                 for (int tt = t; tt < a.T; ++tt)
-                    ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * N + b * HW), vpix, 0u, qn);
+                    ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b * HW), vpix, 0u, qn);
                 ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, qn);
             }
             return;
@@ -375,34 +457,44 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 
         // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
         // (written by other parts in this launch), conf' by plain loads (invariant)
-        const T *p_in = p_all + (size_t)(t - 1) * N + b * HW;
+        const T *p_in = p_all + (size_t)(t - 1) * a.tstride + b * HW;
         const rsrc_t rp = make_rsrc(p_in);
         // t >= 2: the own quads are in the window already (written back below), so
         // only the other parts' quads are loaded
-        const int nown = t >= 2 ? iown1 - iown0 : 0;
-        const int nsq_it = (a.dbg & 2u) ? 0 : nsq - nown;
+        const bool rim = t >= 2;
+        const int nsq_it = (a.dbg & 2u) ? 0 : (rim ? nrest : nall);
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
+            int sl[SMAX];
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                const int k = base + s * NT, i = k < iown0 ? k : k + nown;
+                const int k = base + s * NT;
+                int r, c;  // window quad: row, quad column
+                if (!rim || k < nband) {
+                    const int rr = res_div(k, wqn, rwqn);
+                    r = !rim ? ra + rr : (rr < ntop ? ra + rr : r1 + rr - ntop);
+                    c = qa + k - rr * wqn;
+                } else {
+                    const int m = k - nband, rr = res_div(m, side, rside), cc = m - rr * side;
+                    r = r0 + rr;
+                    c = cc < left ? qa + cc : c1 + cc - left;
+                }
+                sl[s] = (r - rlo) * WW + 4 * (c - wq0) + PADX;  // window cell, % 4 == 0
                 if (k < nsq_it) {
-                    const int r = ra + i / W4, c = (i % W4) * 4;
-                    const unsigned go = (unsigned)(r * W + c) * ES;
+                    const unsigned go = (unsigned)(r * W + 4 * c) * ES;
                     ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
                     if (has_conf) ResVec<T>::template load<0>(rcg, go, 0u, cv[s]);
                 }
             }
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                const int k = base + s * NT, i = k < iown0 ? k : k + nown;
+                const int k = base + s * NT;
                 if (k < nsq_it) {
-                    const int r = ra + i / W4, c = (i % W4) * 4;
                     float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
                     if (has_conf) {
                         f.x = f.x * cv[s][0]; f.y = f.y * cv[s][1]; f.z = f.z * cv[s][2]; f.w = f.w * cv[s][3];
                     }
-                    const int li = (r - rlo) * WW + RX + c;  // li % 4 == 0
+                    const int li = sl[s];
                     *reinterpret_cast<float4 *>(&fwin[li]) = f;
                     fwinB[li - 1] = f.x;
                     *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
@@ -421,11 +513,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (k == REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
-                    const float4 ar = akl[K * NT + tid];
-                    const float *c = &fwin[(y - rlo) * WW + x0 + RX];
+                    const float4 ar = akl[K];
+                    const float *c = &fwin[lown];
                     acc[0] += c[0] * ar.x; acc[1] += c[1] * ar.y; acc[2] += c[2] * ar.z; acc[3] += c[3] * ar.w;
                 }
-                const float4 a4 = akl[k * NT + tid];
+                const float4 a4 = akl[k];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -434,7 +526,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
                     const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
                     const float2 *sp = reinterpret_cast<const float2 *>(fwin + idx);
-                    const float2 s01 = sp[0], s23 = sp[WW / 2];
+                    const float2 s01 = sp[0], s23 = *reinterpret_cast<const float2 *>(fwin + idx + WW);
                     const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                     acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
                 }
@@ -445,17 +537,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // shares no registers with the branch-free path (no spills around it).
             if (kResGeneralPath && wave_fb && has_fb) {
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+                int tq = tid;  // the own quad's row and first column, recomputed (not live across the loop)
+                asm volatile("" : "+v"(tq));
+                const int gr = tq / nqw, y = r0 + gr, x0 = 4 * (c0 + tq - gr * nqw);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float s = 0.f;
 #pragma unroll 1
                     for (int k = 0; k < K; ++k) {
                         if (k == REF) {
-                            const float4 ar = akl[K * NT + tid];
+                            const float4 ar = akl[K];
                             const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
-                            s += fwin[(y - rlo) * WW + x0 + e + RX] * arv[e];
+                            s += fwin[lown + e] * arv[e];
                         }
-                        const float4 a4 = akl[k * NT + tid];
+                        const float4 a4 = akl[k];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
                         const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
                         const float h_im = (float)(y - PH + i) +
@@ -468,9 +563,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                             const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
                             const float hh = 1.f - lh, hw = 1.f - lw;
                             const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                            const int ry = h_low - rlo, rx = w_low + RX;
-                            if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
-                                const float *sp = &fwin[ry * WW + rx];
+                            if ((unsigned)(h_low - rlo) < (unsigned)(WH - 1) &&
+                                (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)) {
+                                const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
                                 v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
                             } else {
                                 const int h_high = h_low + 1, w_high = w_low + 1;
@@ -495,6 +590,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
             float o[4], fin[4];
+            const float4 d4 = akl[K + 2];
+            const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float vv = acc[e];
@@ -506,7 +603,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 o[e] = vv;
                 fin[e] = clip ? vv : clamp0(vv);  // :375-377
             }
-            T *p_out = p_out_all + (size_t)t * N + b * HW;
+            T *p_out = p_out_all + (size_t)t * a.tstride + b * HW;
             ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);
 #pragma unroll
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
@@ -518,20 +615,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0) __hip_atomic_store(&sync[blockIdx.x], (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0)
+            __hip_atomic_store(&sync[1 + blockIdx.x], a.epoch + (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
         // this iteration is done: the barrier above), as the next staging would load it
         if (t < a.T - 1 && active && !(a.dbg & 2u)) {
-            const float4 cw = akl[(K + 1) * NT + tid];
+            const float4 cw = akl[K + 1];
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
             if (has_conf) {
                 f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
             }
-            const int li = (y - rlo) * WW + RX + x0;
-            *reinterpret_cast<float4 *>(&fwin[li]) = f;
-            fwinB[li - 1] = f.x;
-            *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f.y, f.z);
-            fwinB[li + 2] = f.w;
+            *reinterpret_cast<float4 *>(&fwin[lown]) = f;
+            fwinB[lown - 1] = f.x;
+            *reinterpret_cast<float2 *>(&fwinB[lown]) = make_float2(f.y, f.z);
+            fwinB[lown + 2] = f.w;
         }
     }
 }

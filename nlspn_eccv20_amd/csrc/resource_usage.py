@@ -43,6 +43,22 @@ def load_build(build_dir: str = BUILD_DIR) -> dict:
     return rows
 
 
+def loop_scratch(asm: str, name: str) -> dict:
+    """Scratch (spill) instructions of kernel `name` in device assembly text (hipcc -S
+    --cuda-device-only), split into those inside a loop (LLVM's `; in Loop:` block
+    comments) and the rest: {"loop": [...], "other": [...]} of instruction lines."""
+    i = asm.index(name + ":")
+    body = asm[i:asm.index(".Lfunc_end", i)]
+    out, in_loop = {"loop": [], "other": []}, False
+    for line in body.splitlines():
+        m = re.match(r"^\.LBB\d+_\d+:(.*)", line)
+        if m:
+            in_loop = "in Loop:" in m.group(1)
+        elif "scratch_" in line:
+            out["loop" if in_loop else "other"].append(line.strip())
+    return out
+
+
 def demangle(names):
     out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")
     return [o.replace("nlspn::", "").replace("void ", "") for o in out[:len(names)]]

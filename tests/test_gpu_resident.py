@@ -78,7 +78,8 @@ def test_resident_engaged_at_c2():
     with _env("1"):
         ok, grid, block, lds = resident_config(8, 228, 304)
         assert ok and grid == 256 and block == 576 and lds > 80 * 1024
-        assert not resident_config(4, 240, 1216)[0]      # C3: parts exceed one workgroup
+        ok, grid, block, lds = resident_config(4, 240, 1216)  # C3: two launches of 2 images x 128 parts
+        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
 
 
@@ -92,6 +93,10 @@ def test_resident_engaged_at_c2():
     (1, 24, 32, 2.0, torch.float32, True, {}),                          # 3 tiny parts
     (32, 40, 64, 2.0, torch.float32, True, {"affinity": "ASS"}),        # many images, 8 parts each
     (3, 50, 100, 4.0, torch.float32, True, {"affinity": "AS"}),         # B not dividing the CU count
+    (4, 240, 1216, 2.0, torch.float32, True, {}),                       # C3: two image groups
+    (5, 240, 1216, 3.0, torch.float32, True, {"always_clip": True}),    # groups of 2, 2, 1
+    (4, 240, 1216, 2.0, torch.float16, True, {}),                       # C3 shape, fp16 storage
+    (2, 120, 2048, 12.0, torch.float32, True, {}),                      # wide image, taps beyond the halo
 ])
 def test_resident_bitexact_vs_steps(B, H, W, sigma, dtype, conf, kw):
     with _env("1"):
@@ -157,7 +162,7 @@ def test_resident_replays_stable_and_no_abort():
             assert torch.equal(o["pred_inter_tensor"], ref), f"replay {i} differs"
             grid = resident_config(8, 228, 304)[1]
             assert grid > 0
-            assert int(plan.outputs["workspace"][grid].item()) == 0, "resident kernel aborted"
+            assert int(plan.outputs["workspace"][0].item()) == 0, "resident kernel aborted"
         plan.close()
 
 
@@ -183,8 +188,28 @@ def test_time_propagate_reports_resident():
         _lib.PRESERVE_INPUT, 3, torch.cuda.current_stream().cuda_stream, ctypes.byref(first), ctypes.byref(rest),
         ctypes.byref(res)))
     os.environ.pop("NLSPN_RESIDENT", None)
-    assert res.value == 1 and first.value > 0 and rest.value > 0
+    assert res.value == 1 and first.value > 0 and rest.value > 0  # one resident launch (one image group)
     plan.close()
+
+
+def test_c3_resident_vs_oracle_and_replays(oracle):
+    """C3 (KITTI B=4) runs iterations 2..T as two back-to-back resident launches of two
+    images each (progress words carried across them by epoch): against the oracle at the
+    north-star bar, and stable over plan replays."""
+    inp, s = _inputs(4, 240, 1216, seed=7240)
+    with _env("1"):
+        plan = PropagationPlan(*inp, prop_time=18)
+        ref = None
+        for i in range(6):
+            o = plan.replay()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = o["pred_inter_tensor"].clone()
+            assert torch.equal(o["pred_inter_tensor"], ref), f"replay {i} differs"
+        plan.check()
+        e = oracle.propagate(s["pred_init"], s["dep"], s["conf"], s["off_aff"][:, 16:], s["off_aff"][:, :16], 4.0)
+        assert rmse(o["pred"].cpu().numpy(), e["pred"]) <= 1e-4
+        plan.close()
 
 
 def test_two_plans_on_two_streams_bit_exact():

@@ -19,22 +19,22 @@ import resource_usage as RU  # noqa: E402
 
 HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # The resident kernel runs at its 168-VGPR cap (768-thread launch bound = 3 waves per
-# SIMD).  Its compile-time-thread-count builds keep the branch-free iteration path free
-# of scratch; the few spill slots left are reloaded only by the rare general path (taps
-# outside the LDS window) and once per iteration by the own-quad write-back.  Variants
-# forced to zero scratch measured 2-3 % slower (same-box A/B), so the cap
-# below only stops spills from growing.
-RESIDENT_SCRATCH_CAP = 40
+# SIMD) with 80 VGPRs of tap geometry held across its iteration loop.  Its few spill
+# slots belong to the setup; inside the loop at most one reload (a staging index) is
+# allowed — checked on the kernel's device assembly, so a spill cannot come back into
+# the loop silently.
+RESIDENT_SCRATCH_CAP = 64   # bytes per lane, every instantiation
+RESIDENT_LOOP_RELOADS = 2   # scratch instructions inside loops, per instantiation
+_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize"]
 
 
 def _rows():
     rows = RU.load_build()
     if any("prop_resident_kernel" in n for n in rows):
         return rows
-    out = subprocess.run(
-        ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-         "-fno-slp-vectorize", "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/nlspn_ru_test.o",
-         os.path.join(CSRC, "nlspn_kern_resident.hip")], capture_output=True, text=True, cwd=CSRC)
+    out = subprocess.run(["/opt/rocm/bin/hipcc", *_FLAGS, "-Rpass-analysis=kernel-resource-usage", "-c", "-o",
+                          "/tmp/nlspn_ru_test.o", os.path.join(CSRC, "nlspn_kern_resident.hip")],
+                         capture_output=True, text=True, cwd=CSRC)
     assert out.returncode == 0, out.stderr[-2000:]
     return RU.parse(out.stderr)
 
@@ -53,16 +53,21 @@ def test_hot_kernels_have_no_scratch():
 
 def test_resident_kernel_registers_and_scratch():
     """The resident kernel's launch bound (768 threads = 3 waves per SIMD) caps it at
-    168 VGPRs; its scratch stays under the cap (see RESIDENT_SCRATCH_CAP) and the
-    one-image (NTC=128) fp32 build has none."""
+    168 VGPRs; its scratch stays under the cap, and its iteration loop holds at most
+    RESIDENT_LOOP_RELOADS scratch instructions (device assembly)."""
     rows = _rows()
     res = {n: r for n, r in rows.items() if "prop_resident_kernel" in n}
     assert res and all(r["VGPRs"] <= 168 and r.get("Occupancy", 0) >= 3 for r in res.values()), res
-    fixed = {n: r for n, r in res.items() if "Li768ELi2ELi0E" not in n}
-    assert fixed, "compile-time thread-count instantiations missing"
-    assert all(r.get("ScratchSize", 0) <= RESIDENT_SCRATCH_CAP for r in fixed.values()), fixed
-    one = [r for n, r in res.items() if n.startswith("_ZN5nlspn20prop_resident_kernelIfLi768ELi2ELi128E")]
-    assert one and one[0].get("ScratchSize", 0) == 0, one
+    assert any("ELi576E" in n for n in res) and any("ELi128E" in n for n in res), "fixed thread-count builds missing"
+    assert all(r.get("ScratchSize", 0) <= RESIDENT_SCRATCH_CAP for r in res.values()), res
+    out = subprocess.run(["/opt/rocm/bin/hipcc", *_FLAGS, "--cuda-device-only", "-S", "-o", "/tmp/nlspn_res_test.s",
+                          os.path.join(CSRC, "nlspn_kern_resident.hip")], capture_output=True, text=True, cwd=CSRC)
+    assert out.returncode == 0, out.stderr[-2000:]
+    with open("/tmp/nlspn_res_test.s") as f:
+        asm = f.read()
+    for name in res:
+        loop = RU.loop_scratch(asm, name)["loop"]
+        assert len(loop) <= RESIDENT_LOOP_RELOADS, (name, loop)
 
 
 @pytest.mark.parametrize("text,expect", [
