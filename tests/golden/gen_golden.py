@@ -17,8 +17,19 @@ offset branch calls it, so offset-mode forward is NOT generated — the referenc
 has no CPU DCN and its CUDA extension cannot be built here).  Nothing on the
 generated paths is substituted.
 
+Round 2 adds two cases that run further reference modules (same stubs, nothing
+substituted on the generated paths):
+  * gru_*:  NLSPNModel.forward with use_GRU=True (no-offset branch): ConvGRU
+    (:386-403), encode_aff / encode_dep / decode_aff (:123-147), _aff_head + _clip_as
+    (:228-250) re-normalising the affinity every iteration (:365-373).  The model is
+    the reference's own constructor (seeded default init, small GRU dims so the
+    fixture stays small), the encoder/decoder heads replaced by constants as above;
+    the GRU-side state_dict entries are stored in the fixture (keys "sd:<name>").
+  * s2d_*:  S2D.forward (:406-462) on seeded sparse depth, with its pool_convs and
+    conv weights and the pool pyramid (captured by a forward hook on pool_convs).
+
 Outputs: tests/golden/*.npz (float32, allow_pickle=False) + manifest.json.
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [--cases gru,s2d]
 """
 from __future__ import annotations
 
@@ -108,14 +119,75 @@ def synth(g, B, H, W, K, *, density=0.05, max_depth=10.0, signed_aff=False, offs
     return pred_init, dep, conf, off_aff
 
 
+def stub_torchvision():
+    """torchvision (absent) is only used to build the ResNet stages (common.py:27-42);
+    empty layer1..layer3 stand in, so only the reference's own modules exist."""
+    tv = sys.modules["torchvision"]
+    stages = lambda pretrained=False: types.SimpleNamespace(  # noqa: E731
+        layer1=nn.Sequential(), layer2=nn.Sequential(), layer3=nn.Sequential())
+    tv.models = types.SimpleNamespace(resnet18=stages, resnet34=stages)
+
+
+GRU_CASES = [  # (name, flags): the GRU loop of nlspnmodel.py:365-373, no-offset branch
+    ("gru_tgass_preserve", dict(affinity="TGASS", preserve_input=True, always_clip=False, conf_prop=True)),
+    ("gru_ass_clip_noconf", dict(affinity="ASS", preserve_input=True, always_clip=True, conf_prop=False)),
+]
+GRU_SHAPE = dict(B=2, H=16, W=24, T=6, hidden=8)
+
+
+def gen_gru(nl, save, seed):
+    stub_torchvision()
+    B, H, W, T, hd = (GRU_SHAPE[k] for k in ("B", "H", "W", "T", "hidden"))
+    for n, (name, kw) in enumerate(GRU_CASES):
+        args = types.SimpleNamespace(
+            prop_kernel=3, affinity_gamma=0.5, prop_time=T, offset=False, use_GRU=True, use_S2D=False,
+            network="resnet34", from_scratch=True, zero_init_aff=False, GRU_hidden_dim=hd, GRU_input_dim=hd,
+            lr=1e-3, max_depth=10.0, patch_height=H, patch_width=W, **kw)
+        torch.manual_seed(seed + n)
+        m = nl.NLSPNModel(args)
+        g = torch.Generator().manual_seed(seed + 100 + n)
+        pred_init, dep, conf, off_aff = synth(g, B, H, W, 8, density=0.1)
+        o = run_forward(m, pred_init, dep, off_aff, conf if kw["conf_prop"] else None)
+        sd = {f"sd:{k}": v for k, v in m.state_dict().items()
+              if k.split(".")[0] in ("GRU", "encode_aff", "encode_dep", "decode_aff", "aff_scale_const")}
+        arrs = dict(pred_init=pred_init, dep=dep, aff_raw=off_aff, pred=o["pred"],
+                    pred_inter=torch.stack(o["pred_inter"], 0), aff=o["aff"], **sd)
+        if kw["conf_prop"]:
+            arrs.update(conf=conf, confidence=o["confidence"])
+        save(name, f"forward with use_GRU=True (ConvGRU hidden/input {hd}), no offset, T={T}, {kw}", **arrs)
+
+
+def gen_s2d(nl, save, seed):
+    for n, (B, H, W, density) in enumerate(((2, 20, 28, 0.08), (1, 13, 17, 0.5))):
+        torch.manual_seed(seed + n)
+        mod = nl.S2D()
+        g = torch.Generator().manual_seed(seed + 100 + n)
+        dep = torch.rand(B, 1, H, W, generator=g) * 10.0
+        dep = dep * (torch.rand(B, 1, H, W, generator=g) < density).float()
+        seen = {}
+        h = mod.pool_convs.register_forward_hook(lambda mm, i, o: seen.update(pyr=i[0].detach()))
+        with torch.no_grad():
+            out = mod(dep)
+        h.remove()
+        sd = {f"sd:{k}": v for k, v in mod.state_dict().items()}
+        save(f"s2d_{H}x{W}", f"S2D.forward (nlspnmodel.py:406-462), B={B}, density={density}",
+             dep=dep, pyramid=seen["pyr"], out=out, **sd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT_DIR)
+    ap.add_argument("--cases", default="all", help="comma list of: base, gru, s2d (default all)")
     a = ap.parse_args()
+    which = {"base", "gru", "s2d"} if a.cases == "all" else set(a.cases.split(","))
     nl = import_reference()
     torch.set_num_threads(1)
+    mpath = os.path.join(a.out, "manifest.json")
     manifest = {"generator": "tests/golden/gen_golden.py", "seed": SEED,
                 "reference": "XJTUXYC/NLSPN_ECCV20 src/model/nlspnmodel.py", "cases": {}}
+    if "base" not in which and os.path.exists(mpath):
+        with open(mpath) as f:
+            manifest = json.load(f)
     g = torch.Generator().manual_seed(SEED)
 
     def save(name, desc, **arrs):
@@ -123,6 +195,16 @@ def main():
         np.savez_compressed(path, **{k: np.ascontiguousarray(v.detach().numpy() if torch.is_tensor(v) else v)
                                      for k, v in arrs.items()})
         manifest["cases"][name] = {"desc": desc, "arrays": {k: list(np.shape(v)) for k, v in arrs.items()}}
+
+    if "gru" in which:
+        gen_gru(nl, save, SEED + 1000)
+    if "s2d" in which:
+        gen_s2d(nl, save, SEED + 2000)
+    if "base" not in which:
+        with open(mpath, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        print(f"wrote {sorted(which)} fixtures")
+        return
 
     # 1) affinity normalisation (:179-201 + :261-269), all kinds, K=8 and K=24.
     for kind in ("AS", "ASS", "TC", "TGASS"):
@@ -184,12 +266,7 @@ def main():
     # 6) NLSPNModel state_dict names/shapes (checkpoint compatibility of the drop-in).
     #    The ResNet stages come from torchvision (absent): a stub returns empty
     #    layer1..layer3 so only the keys the reference itself defines are recorded.
-    tv = sys.modules["torchvision"]
-    tv.models = types.SimpleNamespace(
-        resnet18=lambda pretrained=False: types.SimpleNamespace(layer1=nn.Sequential(), layer2=nn.Sequential(),
-                                                                 layer3=nn.Sequential()),
-        resnet34=lambda pretrained=False: types.SimpleNamespace(layer1=nn.Sequential(), layer2=nn.Sequential(),
-                                                                 layer3=nn.Sequential()))
+    stub_torchvision()
     keys = {}
     for tag, kw in (("gru_s2d_offset", dict(offset=True, use_GRU=True, use_S2D=True, conf_prop=True)),
                     ("plain", dict(offset=False, use_GRU=False, use_S2D=False, conf_prop=True))):
