@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../nlspn_eccv20_amd/csrc/nlspn_step.h"
+#include "step2_exp.h"
 
 using namespace nlspn;
 
@@ -34,12 +35,29 @@ struct Variant {
     std::string name;
     const void *fn;
     int TH, TW, PX;
+    bool persistent = false;  // grid = CUs x resident workgroups (prop_step2_kernel walks tiles)
 };
+
+unsigned grid_of(const Variant &v, int ntiles) {
+    if (!v.persistent) return (unsigned)ntiles;
+    int dev = 0, cus = 0, occ = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, v.TH * v.TW / v.PX, 0));
+    return (unsigned)std::min(ntiles, cus * std::max(occ, 1));
+}
 
 template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool PRE>
 Variant mk(const char *name) {
     return Variant{name, reinterpret_cast<const void *>(&prop_step_kernel<T, KH, KW, TH, TW, PX, RY, RX, SV, true, PRE, false>),
                    TH, TW, PX};
+}
+
+// The pixel-pair kernel (nlspn_step2.h): PX = 2 for the launch shape
+template <typename T, int KH, int KW, int TH, int TW, int RY, int RX, int DBG = 0>
+Variant mk2(const char *name) {
+    return Variant{name, reinterpret_cast<const void *>(&prop_step2_kernel<T, KH, KW, TH, TW, RY, RX, DBG>), TH, TW, 2,
+                   true};
 }
 
 // Memory-only ceiling: the same per-pixel planes (K aff, 2K offsets, dep, p_in,
@@ -113,12 +131,14 @@ template <typename T, int KH, int KW> std::vector<Variant> variants();
 template <> std::vector<Variant> variants<float, 3, 3>() {
     return {
         mk<float, 3, 3, 8, 32, 1, 8, 8, 4, true>("8x32 px1 R8 (product)"),
+        mk2<float, 3, 3, 8, 64, 8, 8>("pair 8x64 R8"),
+        mk2<float, 3, 3, 8, 32, 8, 8>("pair 8x32 R8 (128t)"),
+        mk2<float, 3, 3, 16, 32, 8, 8>("pair 16x32 R8"),
         mk<float, 3, 3, 16, 16, 1, 8, 8, 4, true>("16x16 px1 R8"),
         mk<float, 3, 3, 4, 64, 1, 8, 8, 4, true>("4x64 px1 R8"),
         mk<float, 3, 3, 8, 64, 1, 8, 8, 4, true>("8x64 px1 R8 (512t)"),
         mk<float, 3, 3, 16, 32, 1, 8, 8, 4, true>("16x32 px1 R8 (512t)"),
         mk<float, 3, 3, 4, 32, 1, 8, 8, 4, true>("4x32 px1 R8 (128t)"),
-        mk<float, 3, 3, 8, 32, 1, 8, 8, 4, false>("8x32 px1 R8 nopre"),
         mk<float, 3, 3, 16, 64, 4, 8, 8, 4, true>("16x64 px4 R8"),
         mk<float, 3, 3, 8, 64, 2, 8, 8, 4, true>("8x64 px2 R8"),
         mk<float, 3, 3, 4, 64, 1, 8, 8, 1, true>("4x64 px1 scalar-stage"),
@@ -126,18 +146,24 @@ template <> std::vector<Variant> variants<float, 3, 3>() {
 }
 template <> std::vector<Variant> variants<__half, 1, 17>() {
     return {
-        mk<__half, 1, 17, 8, 32, 1, 8, 16, 4, true>("8x32 px1 (product)"),
+        mk<__half, 1, 17, 8, 32, 1, 8, 16, 4, true>("8x32 px1 (round 1)"),
+        mk2<__half, 1, 17, 8, 64, 8, 16>("pair 8x64 (product)"),
+        mk2<__half, 1, 17, 4, 128, 8, 16>("pair 4x128"),
+        mk2<__half, 1, 17, 16, 32, 8, 16>("pair 16x32"),
+        mk2<__half, 1, 17, 8, 32, 8, 16>("pair 8x32 (128t)"),
+        mk2<__half, 1, 17, 8, 128, 8, 16>("pair 8x128 (512t)"),
+        mk2<__half, 1, 17, 16, 32, 8, 16, 1>("pair 16x32 DBG nostage"),
+        mk2<__half, 1, 17, 16, 32, 8, 16, 2>("pair 16x32 DBG notaps"),
+        mk2<__half, 1, 17, 16, 32, 8, 16, 3>("pair 16x32 DBG neither"),
         mk<__half, 1, 17, 16, 16, 1, 8, 16, 4, true>("16x16 px1"),
         mk<__half, 1, 17, 4, 64, 1, 8, 16, 4, true>("4x64 px1"),
         mk<__half, 1, 17, 8, 64, 1, 8, 16, 4, true>("8x64 px1 (512t)"),
         mk<__half, 1, 17, 4, 32, 1, 8, 16, 4, true>("4x32 px1 (128t)"),
-        mk<__half, 1, 17, 8, 32, 1, 8, 16, 4, false>("8x32 px1 nopre"),
         mk<__half, 1, 17, 8, 32, 1, 4, 12, 4, true>("8x32 px1 RY4 RX12"),
         mk<__half, 1, 17, 8, 64, 2, 8, 16, 4, true>("8x64 px2"),
         mk<__half, 1, 17, 4, 64, 2, 8, 16, 4, true>("4x64 px2 (128t)"),
         mk<__half, 1, 17, 16, 32, 2, 8, 16, 4, true>("16x32 px2"),
         mk<__half, 1, 17, 8, 32, 2, 8, 16, 4, true>("8x32 px2 (128t)"),
-        mk<__half, 1, 17, 8, 64, 2, 8, 16, 4, false>("8x64 px2 nopre"),
         mk<__half, 1, 17, 4, 64, 4, 8, 16, 4, true>("4x64 px4 (64t)"),
     };
 }
@@ -201,7 +227,7 @@ int run(int B, int H, int W, int reps, int rounds, float sigma) {
         StepArgs a = args_for(vs[vi]);
         void *kargs[] = {&a};
         CK(hipMemset(dout, 0, N * ES));
-        CK(hipLaunchKernel(vs[vi].fn, dim3(B * a.tiles_x * a.tiles_y), dim3(vs[vi].TH * vs[vi].TW / vs[vi].PX), kargs, 0, s));
+        CK(hipLaunchKernel(vs[vi].fn, dim3(grid_of(vs[vi], B * a.tiles_x * a.tiles_y)), dim3(vs[vi].TH * vs[vi].TW / vs[vi].PX), kargs, 0, s));
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(vi == 0 ? ref.data() : got.data(), dout, N * ES, hipMemcpyDeviceToHost));
         if (vi > 0) {
@@ -263,7 +289,7 @@ int run(int B, int H, int W, int reps, int rounds, float sigma) {
             StepArgs a = args_for(vs[vi]);
             void *kargs[] = {&a};
             for (int i = 0; i < reps; ++i)
-                CK(hipExtLaunchKernel(vs[vi].fn, dim3(B * a.tiles_x * a.tiles_y), dim3(vs[vi].TH * vs[vi].TW / vs[vi].PX),
+                CK(hipExtLaunchKernel(vs[vi].fn, dim3(grid_of(vs[vi], B * a.tiles_x * a.tiles_y)), dim3(vs[vi].TH * vs[vi].TW / vs[vi].PX),
                                       kargs, 0, s, ev[2 * i], ev[2 * i + 1], 0));
             CK(hipStreamSynchronize(s));
             double sum = 0;
