@@ -35,6 +35,7 @@ extern "C" {
 /* element type of every tensor argument (math is always fp32) */
 #define NLSPN_DTYPE_F32 0
 #define NLSPN_DTYPE_F16 1
+#define NLSPN_DTYPE_F64 2 /* the seam-2 DCN entry points only (nlspn_mdcn_forward/backward) */
 
 /* affinity normalisation kinds, src/config.py:259-263 / nlspnmodel.py:179-201 */
 #define NLSPN_AFF_AS 0
@@ -231,7 +232,8 @@ int nlspn_affinity_normalize_backward(int dtype, const void *aff_raw, int64_t af
  * Modulated DCNv2 forward, seam 2 of the drop-in (the `DCN` pybind module,
  * src/model/deformconv/src/vision.cpp:9, modulated_deform_conv.h:10-44,
  * cuda/modulated_deform_conv_cuda.cu:19-121), as one direct (GEMM-free) gather
- * kernel.  All tensors contiguous NCHW.
+ * kernel.  dtype: float32, float16 (float arithmetic) or float64 (double
+ * arithmetic, .cu:93's AT_DISPATCH_FLOATING_TYPES).  All tensors contiguous NCHW.
  *   input (B,C,H,W), weight (Cout, C/group, kh, kw), bias (Cout) or NULL,
  *   offset (B, 2*dg*kh*kw, Ho, Wo), mask (B, dg*kh*kw, Ho, Wo),
  *   output (B, Cout, Ho, Wo) with Ho = (H + 2ph - (dh(kh-1)+1))/sh + 1 (.cu:75-76).
@@ -247,9 +249,11 @@ int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const v
 /*
  * Modulated DCNv2 backward, seam 2 (DCN.modulated_deform_conv_backward,
  * src/model/deformconv/src/vision.cpp:10, modulated_deform_conv.h:46-86,
- * cuda/modulated_deform_conv_cuda.cu:124-280), float32.  Same layouts as
+ * cuda/modulated_deform_conv_cuda.cu:124-280), float32 or float64 (dtype
+ * NLSPN_DTYPE_F64: double arithmetic throughout, as the reference's
+ * AT_DISPATCH_FLOATING_TYPES at .cu:221 — what gradcheck runs in).  Same layouts as
  * nlspn_mdcn_forward; grad_output (B, Cout, Ho, Wo).  Writes grad_input (zeroed
- * here, then scattered with float atomics as the reference's col2im, so its last
+ * here, then scattered with atomics as the reference's col2im, so its last
  * bits depend on arrival order), grad_offset, grad_mask, grad_weight and — if
  * non-NULL — grad_bias.  Reproduces the reference's col2im call passing pad_h for
  * pad_w (.cuh:371): identical results for square padding, the reference's own

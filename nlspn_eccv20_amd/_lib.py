@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NLSPN_LIB_PATH") or os.path.join(_HERE, "lib", "libnlspn_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nlspn_prop.h")
 
-DTYPE_F32, DTYPE_F16 = 0, 1
+DTYPE_F32, DTYPE_F16, DTYPE_F64 = 0, 1, 2  # F64: the seam-2 DCN entry points only
 AFF_KINDS = {"AS": 0, "ASS": 1, "TC": 2, "TGASS": 3}
 PRESERVE_INPUT, ALWAYS_CLIP = 0x1, 0x2
 OFF_INSERTED, OFF_RAW = 0, 1

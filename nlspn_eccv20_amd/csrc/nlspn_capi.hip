@@ -559,6 +559,29 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
 
 }  // namespace
 
+namespace {
+// The two DCN backward launches (nlspn_mdcn.h) in arithmetic type A (float or double).
+template <typename A>
+int mdcn_backward_impl(const void *input, const void *weight, const void *offset, const void *mask,
+                       const void *grad_output, void *grad_input, void *grad_offset, void *grad_mask, void *grad_weight,
+                       void *grad_bias, int B, int C, int H, int W, int Cout, int kh, int kw, int sh, int sw, int ph,
+                       int pw, int dh, int dw, int group, int dg, int Ho, int Wo, long long nd, long long nw,
+                       hipStream_t s) {
+    MdcnBwdArgs<A> a{static_cast<const A *>(input), static_cast<const A *>(weight), static_cast<const A *>(offset),
+                     static_cast<const A *>(mask), static_cast<const A *>(grad_output), static_cast<A *>(grad_input),
+                     static_cast<A *>(grad_offset), static_cast<A *>(grad_mask), static_cast<A *>(grad_weight),
+                     static_cast<A *>(grad_bias), B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, group, dg, Ho, Wo};
+    NLSPN_HIP_TRY(hipMemsetAsync(grad_input, 0, sizeof(A) * (size_t)B * C * H * W, s));
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<A>), dim3(elementwise_grid(nd)),
+                                  dim3(256), args, 0, s));
+    if (int rc = check_launch("nlspn_mdcn_backward data")) return rc;
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_weight_kernel<A>), dim3((unsigned)nw),
+                                  dim3(256), args, 0, s));
+    return check_launch("nlspn_mdcn_backward weight");
+}
+}  // namespace
+
 extern "C" {
 
 int nlspn_abi_version(void) { return NLSPN_ABI_VERSION; }
@@ -717,7 +740,8 @@ int nlspn_plan_destroy(nlspn_plan_t plan) {
 int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const void *bias, const void *offset,
                        const void *mask, void *output, int B, int C, int H, int W, int Cout, int kh, int kw, int sh,
                        int sw, int ph, int pw, int dh, int dw, int group, int deformable_group, void *stream) {
-    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16 && dtype != NLSPN_DTYPE_F64)
+        return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
     if (!input || !weight || !offset || !mask || !output) return fail(NLSPN_EINVAL, "null required pointer");
     if (B < 1 || C < 1 || H < 1 || W < 1 || Cout < 1 || kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 ||
         group < 1 || deformable_group < 1 || ph < 0 || pw < 0)
@@ -731,8 +755,9 @@ int nlspn_mdcn_forward(int dtype, const void *input, const void *weight, const v
     if (Ho < 1 || Wo < 1) return fail(NLSPN_EINVAL, "output size %dx%d is empty", Ho, Wo);
     MdcnArgs a{input, weight, bias, offset, mask, output, B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                group, deformable_group, Ho, Wo};
-    const void *fn = dtype == NLSPN_DTYPE_F32 ? reinterpret_cast<const void *>(&mdcn_forward_kernel<float>)
-                                              : reinterpret_cast<const void *>(&mdcn_forward_kernel<__half>);
+    const void *fn = dtype == NLSPN_DTYPE_F32   ? reinterpret_cast<const void *>(&mdcn_forward_kernel<float, float>)
+                     : dtype == NLSPN_DTYPE_F64 ? reinterpret_cast<const void *>(&mdcn_forward_kernel<double, double>)
+                                                : reinterpret_cast<const void *>(&mdcn_forward_kernel<__half, float>);
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(elementwise_grid((long long)B * Cout * Ho * Wo)), dim3(256), args, 0,
                                   as_stream(stream)));
@@ -744,7 +769,8 @@ int nlspn_mdcn_backward(int dtype, const void *input, const void *weight, const 
                         void *grad_weight, void *grad_bias, int B, int C, int H, int W, int Cout, int kh, int kw,
                         int sh, int sw, int ph, int pw, int dh, int dw, int group, int deformable_group,
                         void *stream) {
-    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "the DCN backward is implemented for float32");
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F64)
+        return fail(NLSPN_EUNSUPPORTED, "the DCN backward is implemented for float32 and float64");
     if (!input || !weight || !offset || !mask || !grad_output || !grad_input || !grad_offset || !grad_mask ||
         !grad_weight)
         return fail(NLSPN_EINVAL, "null required pointer");
@@ -758,24 +784,16 @@ int nlspn_mdcn_backward(int dtype, const void *input, const void *weight, const 
     const int Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1;
     const int Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
     if (Ho < 1 || Wo < 1) return fail(NLSPN_EINVAL, "output size %dx%d is empty", Ho, Wo);
-    hipStream_t s = as_stream(stream);
-    MdcnBwdArgs a{static_cast<const float *>(input), static_cast<const float *>(weight),
-                  static_cast<const float *>(offset), static_cast<const float *>(mask),
-                  static_cast<const float *>(grad_output), static_cast<float *>(grad_input),
-                  static_cast<float *>(grad_offset), static_cast<float *>(grad_mask), static_cast<float *>(grad_weight),
-                  static_cast<float *>(grad_bias), B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, group,
-                  deformable_group, Ho, Wo};
-    NLSPN_HIP_TRY(hipMemsetAsync(grad_input, 0, sizeof(float) * (size_t)B * C * H * W, s));
-    void *args[] = {&a};
-    const long long nd = (long long)B * deformable_group * kh * kw * Ho * Wo;
-    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel), dim3(elementwise_grid(nd)),
-                                  dim3(256), args, 0, s));
-    if (int rc = check_launch("nlspn_mdcn_backward data")) return rc;
     const long long nw = (long long)Cout * (C / group) * kh * kw + (grad_bias ? Cout : 0);
     if (nw > 0x7fffffffLL) return fail(NLSPN_EINVAL, "too many weight elements");
-    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&mdcn_bwd_weight_kernel), dim3((unsigned)nw),
-                                  dim3(256), args, 0, s));
-    return check_launch("nlspn_mdcn_backward weight");
+    const long long nd = (long long)B * deformable_group * kh * kw * Ho * Wo;
+    return dtype == NLSPN_DTYPE_F64
+               ? mdcn_backward_impl<double>(input, weight, offset, mask, grad_output, grad_input, grad_offset, grad_mask,
+                                            grad_weight, grad_bias, B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+                                            group, deformable_group, Ho, Wo, nd, nw, as_stream(stream))
+               : mdcn_backward_impl<float>(input, weight, offset, mask, grad_output, grad_input, grad_offset, grad_mask,
+                                           grad_weight, grad_bias, B, C, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+                                           group, deformable_group, Ho, Wo, nd, nw, as_stream(stream));
 }
 
 int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const void *dep, const void *aff,

@@ -15,7 +15,18 @@ from torch.autograd.function import once_differentiable
 from torch.nn.modules.utils import _pair
 
 from . import _lib
-from .propagation import _cuda, _dtype_code, _ptr, _stream
+from .propagation import _cuda, _ptr, _stream
+
+_DCN_DTYPES = {torch.float32: _lib.DTYPE_F32, torch.float16: _lib.DTYPE_F16, torch.float64: _lib.DTYPE_F64}
+
+
+def _dcn_dtype(t: torch.Tensor, backward: bool = False) -> int:
+    """float32 / float64 (the reference's AT_DISPATCH_FLOATING_TYPES, .cu:93 / .cu:221);
+    float16 storage for the forward (float arithmetic)."""
+    if t.dtype not in _DCN_DTYPES or (backward and t.dtype == torch.float16):
+        raise NotImplementedError(f"modulated_deform_conv_{'backward' if backward else 'forward'}: "
+                                  f"dtype {t.dtype} is not supported")
+    return _DCN_DTYPES[t.dtype]
 
 __all__ = ["modulated_deform_conv_forward", "modulated_deform_conv_backward", "ModulatedDeformConvFunction"]
 
@@ -54,7 +65,7 @@ def modulated_deform_conv_forward(input, weight, bias, offset, mask, kernel_h, k
     out = torch.empty((B, Cout, Ho, Wo), dtype=dt, device=input.device)
     with torch.cuda.device(input.device):
         _lib.check(_lib.get().nlspn_mdcn_forward(
-            _dtype_code(input), _ptr(input), _ptr(weight), _ptr(bias), _ptr(offset), _ptr(mask), _ptr(out),
+            _dcn_dtype(input), _ptr(input), _ptr(weight), _ptr(bias), _ptr(offset), _ptr(mask), _ptr(out),
             B, C, H, W, Cout, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
             group, deformable_group, _stream(input.device)))
     return out
@@ -65,9 +76,9 @@ def modulated_deform_conv_backward(input, weight, bias, offset, mask, grad_outpu
                                    im2col_step):
     """Same signature, checks and return list as modulated_deform_conv_cuda_backward
     (modulated_deform_conv_cuda.cu:124-280): [grad_input, grad_offset, grad_mask,
-    grad_weight, grad_bias].  float32 (the reference also dispatches float64; the
-    MI355X build is float32).  Like the reference's col2im call (.cuh:371) grad_input
-    uses pad_h for the width padding too (identical for square padding)."""
+    grad_weight, grad_bias].  float32 or float64, as the reference dispatches
+    (.cu:221).  Like the reference's col2im call (.cuh:371) grad_input uses pad_h for
+    the width padding too (identical for square padding)."""
     if not input.is_contiguous():
         raise RuntimeError("input tensor has to be contiguous")
     if not weight.is_contiguous():
@@ -75,8 +86,10 @@ def modulated_deform_conv_backward(input, weight, bias, offset, mask, grad_outpu
     for n, t in (("input", input), ("weight", weight), ("bias", bias), ("offset", offset), ("mask", mask),
                  ("grad_output", grad_output)):
         _cuda(n, t)
-    if input.dtype != torch.float32:
-        raise NotImplementedError("modulated_deform_conv_backward: float32 only on MI355X")
+    dt = _dcn_dtype(input, backward=True)
+    for n, t in (("weight", weight), ("bias", bias), ("offset", offset), ("mask", mask), ("grad_output", grad_output)):
+        if t is not None and t.dtype != input.dtype:
+            raise RuntimeError(f"{n} dtype {t.dtype} differs from input dtype {input.dtype}")
     B, C, H, W = input.shape
     Cout, Ckern, kh_, kw_ = weight.shape
     if (C % group) != 0 or (Cout % group) != 0:
@@ -102,7 +115,7 @@ def modulated_deform_conv_backward(input, weight, bias, offset, mask, grad_outpu
     grad_bias = torch.empty_like(bias) if bias is not None else None
     with torch.cuda.device(input.device):
         _lib.check(_lib.get().nlspn_mdcn_backward(
-            _lib.DTYPE_F32, _ptr(input), _ptr(weight), _ptr(offset), _ptr(mask), _ptr(grad_output),
+            dt, _ptr(input), _ptr(weight), _ptr(offset), _ptr(mask), _ptr(grad_output),
             _ptr(grad_input), _ptr(grad_offset), _ptr(grad_mask), _ptr(grad_weight), _ptr(grad_bias),
             B, C, H, W, Cout, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
             group, deformable_group, _stream(input.device)))

@@ -98,3 +98,53 @@ def test_dcn_backward_errors():
         dcn.modulated_deform_conv_backward(x, w, None, torch.zeros(1, 18, 8, 8, device=DEV),
                                            torch.zeros(1, 9, 8, 8, device=DEV), torch.zeros(1, 4, 8, 8, device=DEV),
                                            3, 3, 1, 1, 1, 1, 1, 1, 2, 1, 64)
+
+
+# ------------------------------------------------------------------ float64 (seam 2)
+# The reference dispatches float and double (AT_DISPATCH_FLOATING_TYPES, .cu:93 / .cu:221);
+# the float64 kernels do double arithmetic throughout, so they meet the fp64 oracle to
+# ~1e-12 relative (forward) — the only differences are summation order — and the
+# reference-style gradcheck (deformconv/test.py:405-434, run here in float64 as
+# torch.autograd.gradcheck expects) passes through ModulatedDeformConvFunction.
+@pytest.mark.parametrize("case", CASES)
+def test_dcn_float64_vs_oracle(oracle, case):
+    C, Cout, group, dg, kh, kw, stride, pad, dil = case
+    args64 = [x.astype(np.float64) for x in _case(3, *case)]
+    inp, wt, bias, off, mask = (cu(x) for x in args64)
+    out = dcn.modulated_deform_conv_forward(inp, wt, bias, off, mask, kh, kw, *stride, *pad, *dil, group, dg, 64)
+    assert out.dtype == torch.float64
+    exp = oracle.mdcn_forward(*args64, stride, pad, dil, group, dg)
+    assert rel(out.cpu().numpy(), exp) <= 1e-12
+    g = np.random.default_rng(4).standard_normal(out.shape)
+    got = dcn.modulated_deform_conv_backward(inp, wt, bias, off, mask, cu(g), kh, kw, *stride, *pad, *dil, group,
+                                             dg, 64)
+    ref = oracle.mdcn_backward(args64[0], args64[1], args64[3], args64[4], g, stride, pad, dil, group, dg)
+    for gt, rt in zip(got, ref):
+        assert gt.dtype == torch.float64 and rel(gt.cpu().numpy(), rt) <= 1e-10
+
+
+def test_dcn_gradcheck_float64():
+    """torch.autograd.gradcheck of ModulatedDeformConvFunction in float64, the reference's
+    check_gradient_mdconv setup (test.py:15-18, 405-434: N=2, inC=4, 4x4, outC=4, 3x3,
+    groups 2, stride 1, padding 1)."""
+    torch.manual_seed(0)
+    N, inC, inH, inW, outC, kH, kW, dgr = 2, 4, 4, 4, 4, 3, 3, 1
+    d = dict(dtype=torch.float64, device=DEV)
+    inp = (torch.rand(N, inC, inH, inW, **d) * 0.01).requires_grad_()
+    off = (torch.randn(N, dgr * 2 * kW * kH, inH, inW, **d) * 2).requires_grad_()
+    mask = torch.sigmoid(torch.rand(N, dgr * kW * kH, inH, inW, **d)).detach().requires_grad_()
+    wt = torch.randn(outC, inC // 2, kH, kW, **d).requires_grad_()
+    bias = torch.rand(outC, **d).requires_grad_()
+    assert torch.autograd.gradcheck(dcn.ModulatedDeformConvFunction.apply,
+                                    (inp, off, mask, wt, bias, 1, 1, 1, 2, dgr, 1),
+                                    eps=1e-6, atol=1e-5, rtol=1e-4, raise_exception=True,
+                                    nondet_tol=1e-12)  # grad_input: an atomic scatter, as the reference's col2im
+
+
+def test_dcn_rejects_float16_backward():
+    x = torch.zeros((1, 1, 4, 4), dtype=torch.float16, device=DEV)
+    w = torch.ones((1, 1, 3, 3), dtype=torch.float16, device=DEV)
+    with pytest.raises(NotImplementedError):
+        dcn.modulated_deform_conv_backward(x, w, None, torch.zeros((1, 18, 4, 4), dtype=torch.float16, device=DEV),
+                                           torch.ones((1, 9, 4, 4), dtype=torch.float16, device=DEV), x,
+                                           3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 64)
