@@ -116,9 +116,9 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
                     void *p_out, void *pred_out,
                     int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
 
-/* Bytes of device workspace nlspn_propagate uses: the resident kernel's progress
- * words (one 32-bit word per workgroup + an abort word at index grid).  With a
- * NULL workspace nlspn_propagate runs iterations 2..T as T-1 launches instead. */
+/* Bytes of device workspace nlspn_propagate uses: the resident kernel's abort word
+ * (index 0) and progress words (one 32-bit word per workgroup, from index 1).  With
+ * a NULL workspace nlspn_propagate runs iterations 2..T as T-1 launches instead. */
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
 
 /*
@@ -126,12 +126,14 @@ size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
  *   step 1   : the prologue fused into the first iteration — _off_insert (:324)
  *              if off_out, _affinity_normalization (:325), mask_fix / confidence
  *              blend (:328-334), first blend+clamp (:341-348), then iteration 1
- *   steps 2..T: ONE resident launch (the invariant planes held on chip for all
- *              iterations, per-workgroup progress words in `workspace`) when the
- *              geometry allows it (3x3 learned offsets, W % 4 == 0, 16-B aligned
- *              planes, every part fits a workgroup: nlspn_resident_config), else
- *              T-1 nlspn_prop_step launches; pred_inter[t] each, the last also pred.
- *              Both forms are bit-identical.
+ *   steps 2..T: resident launches — the invariant planes held on chip for all
+ *              iterations, one launch per image group (C2: all 8 NYU images in one;
+ *              C3: the 4 KITTI images as two launches of 2), per-workgroup progress
+ *              words in `workspace` — when the geometry allows it (3x3 learned
+ *              offsets, W % 4 == 0, 16-B aligned planes, every rectangular part fits
+ *              a workgroup: nlspn_resident_config), else T-1 nlspn_prop_step
+ *              launches; pred_inter[t] each, the last also pred.  Both forms are
+ *              bit-identical.
  * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
  *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
  *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
@@ -151,10 +153,9 @@ int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const voi
 /*
  * Plans: nlspn_propagate captured once into a hipGraph (T kernel nodes) and
  * replayed with one hipGraphLaunch.  Pointers are baked in at creation; γ stays
- * live because it is read from device memory.  A plan of at most two launches
- * (step 1 + the resident kernel) re-issues its recorded launches directly
- * instead, which costs less than a graph launch; NLSPN_PLAN_GRAPH=1 forces the
- * graph.
+ * live because it is read from device memory.  A resident plan (step 1 + the
+ * resident launches) re-issues its recorded launches directly instead, which
+ * costs less than a graph launch; NLSPN_PLAN_GRAPH=1 forces the graph.
  */
 typedef struct nlspn_plan *nlspn_plan_t;
 int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, const void *dep,
@@ -282,8 +283,9 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
 /*
  * Diagnostics: run nlspn_propagate `reps` times with dispatch-recorded HIP events
  * around every launch, synchronise, and return the mean duration of step 1
- * (first_ms) and of iterations 2..T (rest_ms: the resident kernel, or the sum of
- * the T-1 step kernels); *resident = 1 if the resident kernel ran.
+ * (first_ms) and of iterations 2..T (rest_ms: from the start of the first
+ * resident launch to the end of the last, or the sum of the T-1 step kernels);
+ * *resident = the number of resident launches (image groups), 0 for step launches.
  */
 int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
                          const void *aff_raw, int64_t aff_bstride, const void *off_raw,
@@ -294,8 +296,9 @@ int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, cons
 
 /*
  * Diagnostics: 1 if nlspn_propagate would run iterations 2..T as the resident
- * kernel for this shape (given 16-B aligned planes and a workspace), with its
- * launch shape; 0 otherwise.  Queries the current device's CU count.
+ * kernel for this shape (given 16-B aligned planes and a workspace), with the
+ * launch shape of its first image group; 0 otherwise.  Queries the current
+ * device's CU count.
  */
 int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf,
                           int *grid, int *block, int *lds_bytes);
