@@ -78,6 +78,20 @@ def kernel_geometry(prop_kernel) -> Tuple[int, int]:
     return int(kh), int(kw)
 
 
+_OPS = None
+
+
+def _torch_ops():
+    """torch.ops.nlspn when the operator layer (libnlspn_torch.so) is built, else None:
+    the ops run the same kernels with ~2.5x less host cost per call than ctypes
+    (tools/op_overhead.py), which matters where a call is issued per iteration (GRU mode)."""
+    global _OPS
+    if _OPS is None:
+        from . import ops
+        _OPS = torch.ops.nlspn if ops.available() else False
+    return _OPS or None
+
+
 def _gamma_f32(gamma) -> torch.Tensor:
     if not torch.is_tensor(gamma):
         raise TypeError("gamma must be a device tensor (aff_scale_const)")
@@ -139,6 +153,9 @@ def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "
     (float32) in aff and, for TGASS, gamma."""
     if torch.is_grad_enabled() and (aff.requires_grad or (torch.is_tensor(gamma) and gamma.requires_grad)):
         return _AffNormFn.apply(aff, gamma, kind)
+    top = _torch_ops()
+    if top is not None and aff.is_cuda and torch.is_tensor(gamma) and gamma.is_cuda:
+        return top.affinity_normalization(aff, gamma, kind)
     return _affinity_normalization(aff, gamma, kind)
 
 
@@ -239,6 +256,11 @@ def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optio
             and any(t is not None and t.requires_grad for t in (feat, confidence, aff, offset))):
         return _PropStepFn.apply(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input,
                                  always_clip)
+    top = _torch_ops()
+    if top is not None and out is None and pred_out is None and feat.is_cuda:
+        kh, kw = kernel_geometry(kernel)
+        return top.prop_step(feat, confidence, dep, aff, offset, kh, kw, offset_layout == "raw", preserve_input,
+                             always_clip)
     return _prop_step(feat, confidence, dep, aff, offset, kernel, offset_layout, preserve_input, always_clip, out,
                       pred_out)
 
