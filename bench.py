@@ -145,10 +145,12 @@ def pmc_traffic(config, kernel):
     with open(path) as f:
         d = json.load(f)
     entries = d.get("kernels", {d.get("kernel", ""): d})
-    for name, e in entries.items():
-        if kernel in name:
-            return e.get("hbm_bytes_per_launch")
-    return None
+    # the matching kernel launched most often: the per-iteration step kernel rather than
+    # step 1 (which shares its name), the resident launches of every image group
+    hits = [e for name, e in entries.items() if kernel in name and e.get("hbm_bytes_per_launch")]
+    if not hits:
+        return None
+    return max(hits, key=lambda e: e.get("launches", 0)).get("hbm_bytes_per_launch")
 
 
 def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
@@ -177,10 +179,14 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
     alg = es * (4 + 3 * K) * npx * alg_iters
     sec = ((3 * K + 3) + (T + 3 * K + 5)) * plane
     traffic = pmc_traffic(name, kname)
+    if traffic and resident:
+        traffic *= resident  # per launch -> the section's iterations 2..T (one launch per image group)
     return {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kdesc,
-        "bytes_basis": "compulsory bytes per launch (each plane the launch must read or write, once)",
+        "bytes_basis": ("compulsory bytes of iterations 2..T over all resident launches (each plane read or "
+                        "written once)" if resident else
+                        "compulsory bytes per launch (each plane the launch must read or write, once)"),
         "compulsory_bytes_per_launch": comp, "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5),
         "traffic_over_compulsory": round(traffic / comp, 3) if traffic else None,
         "alg_8d": {"bytes_per_launch": alg, "pixel_iterations_per_launch": npx * alg_iters,

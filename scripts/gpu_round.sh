@@ -19,8 +19,14 @@ NLSPN_RESIDENT=0 timeout -k 10 300 python bench.py --no-backward --no-gru --no-e
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o bench --output-format csv -- \
     python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru > $O/stats.log 2>&1 || exit 1
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_$C -o run --output-format csv -- \
-      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-backward --no-gru --kernel-reps 5 \
-      > $O/pmc_$C.log 2>&1 || exit 1
+# PMC HBM traffic, one config per pass pair (kernels are shared between configs)
+for CFG in nyu kitti nyu_k16; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_${CFG}_$C -o run --output-format csv -- \
+        python3 $R/bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-backward --no-gru \
+        --no-extra-configs --kernel-reps 5 > $O/pmc_${CFG}_$C.log 2>&1 || exit 1
+  done
+  python3 $R/tools/pmc_summary.py --bench $CFG "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over bench.py --config $CFG (scripts/gpu_round.sh $TAG)" \
+      $O/pmc_$CFG.json $O/pmc_${CFG}_FETCH_SIZE/run_counter_collection.csv $O/pmc_${CFG}_WRITE_SIZE/run_counter_collection.csv \
+      > $O/pmc_$CFG.txt 2>&1 || exit 1
 done

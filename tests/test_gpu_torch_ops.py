@@ -15,6 +15,7 @@ def prop_step(feat, conf, dep, aff, off, offset_layout="inserted", preserve_inpu
     """The host mirror's ctypes path into the C ABI (what the ops must equal)."""
     return _prop_step(feat, conf, dep, aff, off, (3, 3), offset_layout, preserve_input, always_clip)
 
+
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
@@ -107,4 +108,4 @@ def test_ops_raise_on_bad_shapes():
     with pytest.raises(RuntimeError, match="expected"):
         torch.ops.nlspn.propagate(pi, dep, conf, aff[:, :5], off, g, 3)
     with pytest.raises(RuntimeError, match="only odd kernel"):
-        torch.ops.nlspn.prop_step(pi, conf, dep, affinity_normalization(aff, g), off, 2, 3, True, True, False)
+        torch.ops.nlspn.prop_step(pi, conf, dep, affinity_normalization(aff, g, "TGASS"), off, 2, 3, True, True, False)
