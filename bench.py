@@ -147,7 +147,11 @@ def pmc_traffic(config, kernel):
     entries = d.get("kernels", {d.get("kernel", ""): d})
     # the matching kernel launched most often: the per-iteration step kernel rather than
     # step 1 (which shares its name), the resident launches of every image group
-    hits = [e for name, e in entries.items() if kernel in name and e.get("hbm_bytes_per_launch")]
+    def first_step(name):  # prop_step_kernel<..., FIRST=true>: step 1, not the per-iteration kernel
+        return name.split(">")[0].replace(" ", "").endswith(",true") and "prop_step_kernel" in name
+
+    hits = [e for name, e in entries.items()
+            if kernel in name and e.get("hbm_bytes_per_launch") and not first_step(name)]
     if not hits:
         return None
     return max(hits, key=lambda e: e.get("launches", 0)).get("hbm_bytes_per_launch")

@@ -30,3 +30,5 @@ for CFG in nyu kitti nyu_k16; do
       $O/pmc_$CFG.json $O/pmc_${CFG}_FETCH_SIZE/run_counter_collection.csv $O/pmc_${CFG}_WRITE_SIZE/run_counter_collection.csv \
       > $O/pmc_$CFG.txt 2>&1 || exit 1
 done
+# the reference's last head layers on MIOpen (input to the head-epilogue fusion work)
+cd $R && timeout -k 10 180 python tools/head_prof.py > $O/head_prof.json 2> $O/head_prof.err || exit 1
