@@ -82,6 +82,30 @@ int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *
                       int B, int H, int W, void *stream);
 
 /*
+ * Head epilogue: the decoder's last three 3x3 convolutions as one
+ * kernel.  Replaces src/model/nlspnmodel.py:296-315 —
+ *   pred_init  = ReLU(id_dec0(cat(id_fd1, fe1)))      id_dec0      :68
+ *   off_aff    = off_aff_dec0(cat(off_aff_fd1, fe1))  off_aff_dec0 :74 (or :76 without offsets)
+ *   confidence = Sigmoid(cf_dec0(cat(cf_fd1, fe1)))   cf_dec0      :83-86
+ * with the four C-channel sources read in place (no concatenated copies):
+ *   fe1, fd_oa   : B x C x H x W (fe1 and off_aff_fd1), contiguous, device float32
+ *   fd_id, fd_cf : B x C x H x W (id_fd1, cf_fd1) or NULL (that head is skipped)
+ *   wm, wv, bias : the weights packed by nlspn_head_pack_weights (nlspn_head_packed_size)
+ *   off_aff      : B x nout x H x W;  pred_init, conf : B x 1 x H x W (NULL with their source)
+ * Arithmetic: f32 operands and products on the matrix cores, f32 accumulation; only the
+ * summation order differs from a sequential f32 convolution.  C % 16 == 0; float32 only.
+ */
+int nlspn_head_packed_size(int C, int nout, int64_t *wm_floats, int64_t *wv_floats,
+                           int64_t *bias_floats);
+int nlspn_head_pack_weights(const float *w_oa, const float *b_oa, const float *w_id,
+                            const float *b_id, const float *w_cf, const float *b_cf,
+                            float *wm, float *wv, float *bias, int C, int nout, void *stream);
+int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id,
+                        const void *fd_cf, const float *wm, const float *wv,
+                        const float *bias, void *off_aff, void *pred_init, void *conf,
+                        int B, int C, int H, int W, int nout, void *stream);
+
+/*
  * Affinity normalisation + reference-tap insertion.
  * Replaces NLSPNModel._affinity_normalization (src/model/nlspnmodel.py:179-201)
  * followed by _aff_insert (:261-269).

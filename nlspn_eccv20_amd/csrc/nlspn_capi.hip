@@ -20,6 +20,7 @@
 #include "nlspn_step.h"
 #include "nlspn_resident.h"
 #include "nlspn_s2d.h"
+#include "nlspn_heads.h"
 
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
@@ -29,6 +30,14 @@ namespace nlspn {
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128>(ResArgs);
 NLSPN_RES_EXTERN(float)
 NLSPN_RES_EXTERN(__half)
+// defined in nlspn_kern_heads.hip
+#define NLSPN_HD_EXTERN(MB)                                            \
+    extern template __global__ void heads_kernel<MB, true>(HeadsArgs); \
+    extern template __global__ void heads_kernel<MB, false>(HeadsArgs);
+NLSPN_HD_EXTERN(1)
+NLSPN_HD_EXTERN(2)
+NLSPN_HD_EXTERN(3)
+NLSPN_HD_EXTERN(5)
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -602,6 +611,73 @@ int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *
     NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&s2d_pyramid_kernel), dim3((unsigned)grid), dim3(256),
                                   args, 0, as_stream(stream)));
     return check_launch("nlspn_s2d_pyramid");
+}
+
+static int head_mb(int nout) {
+    const int mb = (nout + 2 + 31) / 32;
+    return mb <= 3 ? mb : (mb <= 5 ? 5 : -1);
+}
+
+int nlspn_head_packed_size(int C, int nout, int64_t *wm_floats, int64_t *wv_floats, int64_t *bias_floats) {
+    if (C < 16 || C % 16 || nout < 1) return fail(NLSPN_EINVAL, "head epilogue: C=%d (multiple of 16) nout=%d", C, nout);
+    const int mb = head_mb(nout);
+    if (mb < 0) return fail(NLSPN_EUNSUPPORTED, "head epilogue: nout=%d (at most 158)", nout);
+    if (wm_floats) *wm_floats = 2LL * C * 9 * 32 * mb;
+    if (wv_floats) *wv_floats = 2LL * C * 9;
+    if (bias_floats) *bias_floats = 32LL * mb;
+    return NLSPN_OK;
+}
+
+int nlspn_head_pack_weights(const float *w_oa, const float *b_oa, const float *w_id, const float *b_id,
+                            const float *w_cf, const float *b_cf, float *wm, float *wv, float *bias, int C, int nout,
+                            void *stream) {
+    int64_t nm = 0, nv = 0, nb = 0;
+    if (int rc = nlspn_head_packed_size(C, nout, &nm, &nv, &nb)) return rc;
+    if (!w_oa || !wm || !wv || !bias) return fail(NLSPN_EINVAL, "head epilogue: null pointer");
+    HeadsPackArgs a{w_oa, b_oa, w_id, b_id, w_cf, b_cf, wm, wv, bias, C, nout, (int)nb};
+    const long long n = nm + nv + nb;
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&heads_pack_kernel), dim3((unsigned)((n + 255) / 256)),
+                                  dim3(256), args, 0, as_stream(stream)));
+    return check_launch("nlspn_head_pack_weights");
+}
+
+int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id, const void *fd_cf,
+                        const float *wm, const float *wv, const float *bias, void *off_aff, void *pred_init,
+                        void *conf, int B, int C, int H, int W, int nout, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "head epilogue: float32 only (dtype %d)", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (int rc = nlspn_head_packed_size(C, nout, nullptr, nullptr, nullptr)) return rc;
+    if (!fe1 || !fd_oa || !wm || !wv || !bias || !off_aff) return fail(NLSPN_EINVAL, "head epilogue: null pointer");
+    if ((fd_id == nullptr) != (pred_init == nullptr) || (fd_cf == nullptr) != (conf == nullptr))
+        return fail(NLSPN_EINVAL, "head epilogue: a head's source and output must both be given or both NULL");
+    HeadsArgs a{static_cast<const float *>(fe1), static_cast<const float *>(fd_oa), static_cast<const float *>(fd_id),
+                static_cast<const float *>(fd_cf), wm, wv, bias, static_cast<float *>(off_aff),
+                static_cast<float *>(pred_init), static_cast<float *>(conf), B, C, H, W, nout,
+                (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH};
+    const long long grid = (long long)B * a.tiles_x * a.tiles_y;
+    if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
+    const bool vec = W % 4 == 0 && aligned(fe1, 16) && aligned(fd_oa, 16) && aligned(fd_id, 16) && aligned(fd_cf, 16);
+    const void *fn = nullptr;
+    int lds = 0;
+    switch (head_mb(nout)) {
+#define NLSPN_HD_CASE(MB)                                                                                   \
+    case MB:                                                                                                \
+        fn = vec ? reinterpret_cast<const void *>(&heads_kernel<MB, true>)                                  \
+                 : reinterpret_cast<const void *>(&heads_kernel<MB, false>);                                \
+        lds = (int)sizeof(float) * HdCfg<MB>::LDS_FLOATS;                                                   \
+        break;
+        NLSPN_HD_CASE(1)
+        NLSPN_HD_CASE(2)
+        NLSPN_HD_CASE(3)
+        NLSPN_HD_CASE(5)
+#undef NLSPN_HD_CASE
+        default: return fail(NLSPN_EUNSUPPORTED, "head epilogue: nout=%d", nout);
+    }
+    if (lds > 65536) NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kHdNT), args, (size_t)lds, as_stream(stream)));
+    return check_launch("nlspn_head_epilogue");
 }
 
 int nlspn_affinity_normalize(int dtype, const void *aff_raw, int64_t aff_bstride, const float *gamma,

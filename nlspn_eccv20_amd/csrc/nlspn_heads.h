@@ -1,0 +1,274 @@
+// Head epilogue: the reference's last three 3x3 convolutions of
+// the decoder, nlspnmodel.py:296-315 —
+//   pred_init  = ReLU(id_dec0(cat(id_fd1, fe1)))          (:297, id_dec0 :68)
+//   off_aff    = off_aff_dec0(cat(off_aff_fd1, fe1))      (:301, off_aff_dec0 :74)
+//   confidence = Sigmoid(cf_dec0(cat(cf_fd1, fe1)))       (:313, cf_dec0 :83-86)
+// — as ONE kernel that reads the four C-channel sources (fe1 shared by all three)
+// directly: no torch.cat copies, bias and activation in the epilogue.
+//
+// Implicit GEMM on the f32-input matrix cores (v_mfma_f32_32x32x2_f32: f32 operands,
+// exact f32 products, f32 accumulation — only the summation order differs from a
+// sequential f32 convolution).  D[co][px] = sum_k W[co][k] X[k][px], k = (channel,
+// tap):
+//   * MFMA part, M = 32*MB output channels (0..nout-1 the off_aff conv, nout the
+//     id conv, nout+1 the cf conv, the rest zero), N = 32 pixels of one tile row,
+//     k over fe1 (all columns) and over off_aff_fd1 (off_aff columns only);
+//   * VALU part: the 1-channel id / cf convs' own decoder halves (id_fd1, cf_fd1),
+//     one pixel per thread, weights from scalar registers (wave-uniform loads).
+//     As MFMA columns they would cost 32x their FLOPs.
+// Tile: 8 rows x 32 columns, 256 threads (4 waves, 2 rows each).  The K loop runs
+// over 16-channel chunks: the chunk's input window (16 ch x 10 rows x 40 cols, zero
+// outside the image = the conv's zero padding) and its packed weights are staged in
+// LDS; the next chunk's global loads are in flight in registers while the current
+// chunk computes.
+#pragma once
+
+#include "nlspn_common.h"
+
+namespace nlspn {
+
+constexpr int kHdTH = 8, kHdTW = 32, kHdNT = 256;  // tile rows / columns, threads
+constexpr int kHdCC = 16;                            // channels per K chunk
+constexpr int kHdRS = 40;                            // LDS row stride (cols x0-4 .. x0+35)
+constexpr int kHdCS = (kHdTH + 2) * kHdRS + 16;      // LDS channel stride: 416 = 32 (mod 64) banks
+constexpr int kHdXF4 = kHdCC * (kHdTH + 2) * (kHdRS / 4);  // float4s of one chunk's input window (1600)
+constexpr int kHdXR = (kHdXF4 + kHdNT - 1) / kHdNT;        // per thread (7)
+
+struct HeadsArgs {
+    const float *fe1, *fd_oa, *fd_id, *fd_cf;  // (B,C,H,W) each; fd_id / fd_cf may be null
+    const float *wm;    // packed MFMA weights [2][C][9][32*MB]: source 0 = fe1, 1 = off_aff_fd1
+    const float *wv;    // packed VALU weights [2][C][9]: id conv on id_fd1, cf conv on cf_fd1
+    const float *bias;  // [32*MB]: off_aff biases, id bias, cf bias, zeros
+    float *off_aff;     // (B,nout,H,W)
+    float *pred_init;   // (B,1,H,W) or null
+    float *conf;        // (B,1,H,W) or null
+    int B, C, H, W, nout, tiles_x, tiles_y;
+};
+
+template <int MB> struct HdCfg {
+    static constexpr int NCO = 32 * MB;
+    static constexpr int WCS = 9 * NCO + ((MB % 2) ? 0 : 32);  // LDS weight channel stride: 32 (mod 64) banks
+    static constexpr int WF4 = kHdCC * 9 * NCO / 4;              // float4s of one chunk's weights
+    static constexpr int WR = (WF4 + kHdNT - 1) / kHdNT;
+    static constexpr int LDS_FLOATS = kHdCC * kHdCS + kHdCC * WCS + 2 * kHdTH * kHdTW;
+};
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Chunk q: q < 2*NCH are MFMA chunks (source q / NCH: fe1, off_aff_fd1), then the VALU
+// chunks of id_fd1 and cf_fd1 (those present).
+template <int MB, bool VEC>
+__global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
+    using Cfg = HdCfg<MB>;
+    constexpr int NCO = Cfg::NCO, WCS = Cfg::WCS;
+    extern __shared__ float hd_lds[];
+    float *XL = hd_lds;                       // [16][CS]
+    float *WL = XL + kHdCC * kHdCS;           // [16][WCS]
+    float *SV = WL + kHdCC * WCS;             // [2][256]: the VALU sums per pixel
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int ntile = a.tiles_x * a.tiles_y * a.B;
+    const int tile = xcd_remap(blockIdx.x, ntile);
+    const int b = tile / (a.tiles_x * a.tiles_y), tr = tile - b * a.tiles_x * a.tiles_y;
+    const int ty = tr / a.tiles_x, tx = tr - ty * a.tiles_x;
+    const int y0 = ty * kHdTH, x0 = tx * kHdTW;
+    const int H = a.H, W = a.W, C = a.C;
+    const long long HW = (long long)H * W;
+    const int nch = C / kHdCC;
+    const int nmfma = 2 * nch;
+    const int nvalu = ((a.fd_id != nullptr) + (a.fd_cf != nullptr)) * nch;
+    const int nq = nmfma + nvalu;
+
+    auto source = [&](int q, int &cbase, int &vsrc) __attribute__((always_inline)) -> const float * {
+        if (q < nmfma) {
+            vsrc = -1;
+            cbase = (q % nch) * kHdCC;
+            return q < nch ? a.fe1 : a.fd_oa;
+        }
+        const int v = q - nmfma;
+        cbase = (v % nch) * kHdCC;
+        const bool id_first = a.fd_id != nullptr;
+        vsrc = (v < nch && id_first) ? 0 : 1;
+        return vsrc == 0 ? a.fd_id : a.fd_cf;
+    };
+
+    f32x4 xr[kHdXR];  // ext-vector type: a HIP float4 struct copy from global memory
+    f32x4 wr[Cfg::WR];  // becomes a memcpy that keeps the array in scratch
+    auto load_chunk = [&](int q) __attribute__((always_inline)) {
+        int cbase, vsrc;
+        const float *src = source(q, cbase, vsrc) + ((long long)b * C + cbase) * HW;
+#pragma unroll
+        for (int i = 0; i < kHdXR; ++i) {
+            // every lane loads (clamped, in-bounds address) and zeroes what lies outside
+            // the image afterwards: no divergent branches around the loads, so they stay
+            // in registers and all go out back to back
+            const int f = min(tid + i * kHdNT, kHdXF4 - 1);
+            const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
+            const int row = rem / (kHdRS / 4), c4 = rem - row * (kHdRS / 4);
+            const int y = y0 - 1 + row, x = x0 - 4 + 4 * c4;
+            const bool yin = (unsigned)y < (unsigned)H;
+            const float *p = src + ch * HW + (long long)min(max(y, 0), H - 1) * W;
+            f32x4 v;
+            if (VEC) {
+                v = *reinterpret_cast<const f32x4 *>(p + min(max(x, 0), W - 4));
+                if (!yin || (unsigned)x >= (unsigned)W) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                float e[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    e[j] = p[min(max(x + j, 0), W - 1)];
+                    if (!yin || (unsigned)(x + j) >= (unsigned)W) e[j] = 0.f;
+                }
+                v = f32x4{e[0], e[1], e[2], e[3]};
+            }
+            xr[i] = v;
+        }
+        // weights: loaded (and staged) for VALU chunks too — a redundant copy of a valid
+        // chunk — so that wr is assigned on every path and stays in registers
+        const int wq = q < nmfma ? q : 0;
+        const f32x4 *wsrc = reinterpret_cast<const f32x4 *>(a.wm + ((long long)(wq / nch) * C + (wq % nch) * kHdCC) * 9 * NCO);
+#pragma unroll
+        for (int i = 0; i < Cfg::WR; ++i) wr[i] = wsrc[min(tid + i * kHdNT, Cfg::WF4 - 1)];
+    };
+    auto store_chunk = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kHdXR; ++i) {
+            const int f = tid + i * kHdNT;
+            if (f < kHdXF4) {
+                const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
+                *reinterpret_cast<f32x4 *>(&XL[ch * kHdCS + 4 * rem]) = xr[i];  // rows of 40 = 10 float4
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < Cfg::WR; ++i) {
+            const int f = tid + i * kHdNT;
+            if (f < Cfg::WF4) {
+                const int ch = f / (9 * NCO / 4), rem = f - ch * (9 * NCO / 4);
+                *reinterpret_cast<f32x4 *>(&WL[ch * WCS + 4 * rem]) = wr[i];
+            }
+        }
+    };
+
+    f32x16 acc[MB][2];
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+    float sv_id = 0.f, sv_cf = 0.f;  // VALU sums of this thread's pixel
+    const int vrow = tid >> 5, vcol = tid & 31;
+
+    load_chunk(0);
+    for (int q = 0; q < nq; ++q) {
+        __syncthreads();  // the previous chunk's LDS reads are done
+        store_chunk(q);
+        __syncthreads();
+        if (q + 1 < nq) load_chunk(q + 1);  // in flight while this chunk computes
+        if (q < nmfma) {
+            // B operand: X[k = h][px = l32] of channel 2cp+h at tap (dy,dx), rows 2wv+n
+            const float *xb = XL + h * kHdCS + (2 * wv) * kHdRS + l32 + 3;
+            const float *wb = WL + h * WCS + l32;
+#pragma unroll
+            for (int cp = 0; cp < kHdCC / 2; ++cp) {
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    const int dy = t / 3, dx = t % 3;
+                    float av[MB], bv[2];
+#pragma unroll
+                    for (int m = 0; m < MB; ++m) av[m] = wb[2 * cp * WCS + t * NCO + 32 * m];
+#pragma unroll
+                    for (int n = 0; n < 2; ++n) bv[n] = xb[2 * cp * kHdCS + (n + dy) * kHdRS + dx];
+#pragma unroll
+                    for (int m = 0; m < MB; ++m)
+#pragma unroll
+                        for (int n = 0; n < 2; ++n)
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+                }
+            }
+        } else {
+            int cbase, vsrc;
+            source(q, cbase, vsrc);
+            const float *wvp = a.wv + ((long long)vsrc * C + cbase) * 9;  // wave-uniform: scalar loads
+            const float *xv = XL + vrow * kHdRS + vcol + 3;
+            float s = 0.f;
+#pragma unroll
+            for (int ch = 0; ch < kHdCC; ++ch)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) s += xv[ch * kHdCS + (t / 3) * kHdRS + (t % 3)] * wvp[ch * 9 + t];
+            if (vsrc == 0) sv_id += s; else sv_cf += s;
+        }
+    }
+
+    // epilogue: the VALU sums by pixel, then bias + activation and coalesced row stores
+    SV[tid] = sv_id;
+    SV[kHdNT + tid] = sv_cf;
+    __syncthreads();
+    const int x = x0 + l32;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const int yl = 2 * wv + n, y = y0 + yl;
+        if (y >= H || x >= W) continue;
+        const long long pix = (long long)y * W + x;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = acc[m][n][r] + a.bias[co];
+                if (co < a.nout) {
+                    a.off_aff[((long long)b * a.nout + co) * HW + pix] = v;
+                } else if (co == a.nout) {
+                    if (a.pred_init) {
+                        const float u = v + SV[yl * kHdTW + l32];
+                        a.pred_init[(long long)b * HW + pix] = u < 0.f ? 0.f : u;  // ReLU (NaN kept)
+                    }
+                } else if (co == a.nout + 1) {
+                    if (a.conf) {
+                        const float u = v + SV[kHdNT + yl * kHdTW + l32];
+                        a.conf[(long long)b * HW + pix] = 1.f / (1.f + expf(-u));  // Sigmoid
+                    }
+                }
+            }
+    }
+}
+
+// Packs the three convs' (Cout, 2C, 3, 3) weights and biases into HeadsArgs' layouts.
+// One thread per packed element of wm, then wv and bias.
+struct HeadsPackArgs {
+    const float *w_oa, *b_oa, *w_id, *b_id, *w_cf, *b_cf;  // id / cf may be null
+    float *wm, *wv, *bias;
+    int C, nout, nco;
+};
+
+static __global__ void heads_pack_kernel(HeadsPackArgs a) {
+    const long long nm = 2LL * a.C * 9 * a.nco, nv = 2LL * a.C * 9;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int C2 = 2 * a.C;
+    if (i < nm) {
+        const int co = (int)(i % a.nco);
+        const long long r = i / a.nco;
+        const int t = (int)(r % 9), c = (int)((r / 9) % a.C), s = (int)(r / (9LL * a.C));
+        // input channel of the conv: source 0 = fe1 = channels C..2C-1, source 1 = fd = 0..C-1
+        const int ci = s == 0 ? a.C + c : c;
+        float v = 0.f;
+        if (co < a.nout) v = a.w_oa[((long long)co * C2 + ci) * 9 + t];
+        else if (s == 0 && co == a.nout && a.w_id) v = a.w_id[(long long)ci * 9 + t];
+        else if (s == 0 && co == a.nout + 1 && a.w_cf) v = a.w_cf[(long long)ci * 9 + t];
+        a.wm[i] = v;
+    } else if (i < nm + nv) {
+        const long long j = i - nm;
+        const int t = (int)(j % 9), c = (int)((j / 9) % a.C), s = (int)(j / (9LL * a.C));
+        const float *w = s == 0 ? a.w_id : a.w_cf;
+        a.wv[j] = w ? w[(long long)c * 9 + t] : 0.f;  // the decoder half: input channels 0..C-1
+    } else if (i < nm + nv + a.nco) {
+        const int co = (int)(i - nm - nv);
+        float v = 0.f;
+        if (co < a.nout) v = a.b_oa ? a.b_oa[co] : 0.f;
+        else if (co == a.nout && a.b_id) v = a.b_id[0];
+        else if (co == a.nout + 1 && a.b_cf) v = a.b_cf[0];
+        a.bias[co] = v;
+    }
+}
+
+}  // namespace nlspn

@@ -1,0 +1,15 @@
+// Device code of the head-epilogue convolution kernel (nlspn_heads.h), its own
+// translation unit: built with contraction on (the VALU part's multiply-adds are
+// plain f32 FMAs; the propagation kernels keep -ffp-contract=off for bit parity
+// with the oracle, which this kernel does not claim).  Launched from nlspn_capi.hip.
+#include "nlspn_heads.h"
+
+namespace nlspn {
+#define NLSPN_HD_INST(MB)                                    \
+    template __global__ void heads_kernel<MB, true>(HeadsArgs);  \
+    template __global__ void heads_kernel<MB, false>(HeadsArgs);
+NLSPN_HD_INST(1)
+NLSPN_HD_INST(2)
+NLSPN_HD_INST(3)
+NLSPN_HD_INST(5)
+}  // namespace nlspn

@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from .propagation import affinity_normalization, kernel_geometry, off_insert, prop_step, propagate
+from .heads import HeadWeights, head_epilogue
 from .s2d import s2d_front
 
 __all__ = ["NLSPNModel", "ConvGRU", "S2D", "conv_bn_relu", "convt_bn_relu", "get_resnet18", "get_resnet34", "get",
@@ -244,19 +245,25 @@ class NLSPNModel(nn.Module):
                               relu=False, zero_init=args.zero_init_aff))
         if args.use_S2D:
             self.S2D = S2D()
+        self._head_weights = HeadWeights()  # packed head-epilogue weights (a cache, not state)
         params = nn.ParameterList([p for p in self.parameters() if p.requires_grad])
         self.param_groups = [{"params": params, "lr": args.lr}]
 
     @staticmethod
-    def _concat(fd, fe, dim=1):
-        """nlspnmodel.py:161-177: crop decoder padding, then concatenate."""
+    def _crop(fd, fe):
+        """The decoder-padding crop of nlspnmodel.py:161-174."""
         _, _, Hd, Wd = fd.shape
         _, _, He, We = fe.shape
         if Hd > He:
             fd = fd[:, :, :He, :]
         if Wd > We:
             fd = fd[:, :, :, :We]
-        return torch.cat((fd, fe), dim=dim)
+        return fd
+
+    @classmethod
+    def _concat(cls, fd, fe, dim=1):
+        """nlspnmodel.py:161-177: crop decoder padding, then concatenate."""
+        return torch.cat((cls._crop(fd, fe), fe), dim=dim)
 
     def heads(self, sample):
         """Encoder + decoder heads, nlspnmodel.py:272-315: (pred_init, off_aff, confidence)."""
@@ -272,12 +279,19 @@ class NLSPNModel(nn.Module):
         fd3 = self.dec3(self._concat(fd4, fe4))
         fd2 = self.dec2(self._concat(fd3, fe3))
         id_fd1 = self.id_dec1(self._concat(fd2, fe2))
-        pred_init = self.id_dec0(self._concat(id_fd1, fe1))
         off_aff_fd1 = self.off_aff_dec1(self._concat(fd2, fe2))
+        cf_fd1 = self.cf_dec1(self._concat(fd2, fe2)) if self.args.conf_prop else None
+        if fe1.is_cuda and not torch.is_grad_enabled() and fe1.dtype == torch.float32:
+            # inference: the three last convolutions + bias/activation as one HIP kernel
+            # reading fe1 and the decoder outputs in place (heads.py, nlspn_heads.h)
+            crop = lambda fd: None if fd is None else self._crop(fd, fe1)  # noqa: E731
+            return head_epilogue(fe1, crop(off_aff_fd1), self.off_aff_dec0, crop(id_fd1), self.id_dec0,
+                                 crop(cf_fd1), self.cf_dec0 if self.args.conf_prop else None,
+                                 weights=self._head_weights)
+        pred_init = self.id_dec0(self._concat(id_fd1, fe1))
         off_aff = self.off_aff_dec0(self._concat(off_aff_fd1, fe1))
         confidence = None
         if self.args.conf_prop:
-            cf_fd1 = self.cf_dec1(self._concat(fd2, fe2))
             confidence = self.cf_dec0(self._concat(cf_fd1, fe1))
         return pred_init, off_aff, confidence
 

@@ -245,3 +245,31 @@ def s2d_front(dep, w1, b1, w2, b2):
     h2 = np.maximum(np.einsum("oc,bchw->bohw", w2, h1.astype(np.float64)) +
                     np.asarray(b2, np.float64).reshape(1, 16, 1, 1), 0).astype(np.float32)
     return np.concatenate([h2, d[:, None]], 1), pyr
+
+
+def conv3x3(x, w, b):
+    """3x3 / stride 1 / zero-pad 1 convolution with bias, float64 (nn.Conv2d as the
+    reference's conv_bn_relu(..., bn=False) builds it, common.py:45-67): x (B, Ci, H, W),
+    w (Co, Ci, 3, 3), b (Co) -> (B, Co, H, W)."""
+    x = np.asarray(x, np.float64)
+    w = np.asarray(w, np.float64)
+    B, Ci, H, W = x.shape
+    p = np.pad(x, ((0, 0), (0, 0), (1, 1), (1, 1)))
+    out = np.zeros((B, w.shape[0], H, W), np.float64)
+    for dy in range(3):
+        for dx in range(3):
+            out += np.einsum("oc,bchw->bohw", w[:, :, dy, dx], p[:, :, dy:dy + H, dx:dx + W], optimize=True)
+    return out + np.asarray(b, np.float64).reshape(1, -1, 1, 1)
+
+
+def head_epilogue(fe1, off_aff_fd1, w_oa, b_oa, id_fd1=None, w_id=None, b_id=None, cf_fd1=None, w_cf=None,
+                  b_cf=None):
+    """The decoder's last three heads (src/model/nlspnmodel.py:296-315), float64:
+    pred_init = ReLU(id_dec0(cat(id_fd1, fe1))) (:297), off_aff = off_aff_dec0(cat(
+    off_aff_fd1, fe1)) (:301), confidence = Sigmoid(cf_dec0(cat(cf_fd1, fe1))) (:313).
+    Returns (pred_init or None, off_aff, confidence or None) in float64."""
+    cat = lambda fd: np.concatenate([np.asarray(fd, np.float64), np.asarray(fe1, np.float64)], 1)  # noqa: E731
+    off_aff = conv3x3(cat(off_aff_fd1), w_oa, b_oa)
+    pred_init = None if id_fd1 is None else np.maximum(conv3x3(cat(id_fd1), w_id, b_id), 0.0)
+    conf = None if cf_fd1 is None else 1.0 / (1.0 + np.exp(-conv3x3(cat(cf_fd1), w_cf, b_cf)))
+    return pred_init, off_aff, conf

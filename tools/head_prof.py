@@ -8,10 +8,14 @@ usage: python tools/head_prof.py [--configs nyu,kitti]
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {"nyu": (8, 228, 304), "kitti": (4, 240, 1216)}
 
@@ -63,6 +67,24 @@ def main():
             r["conv_off_aff_ms"] = timed(lambda: oa_dec0(cat))
             r["conv_1ch_ms"] = timed(lambda: cf_dec0(cat))
         macs = B * H * W * 128 * 9 * (3 * args.K + 2)
+        try:
+            from nlspn_eccv20_amd.heads import HeadWeights, head_epilogue
+            hw = HeadWeights()
+            with torch.no_grad():
+                r["fused_ms"] = timed(lambda: head_epilogue(fe1, oa_fd1, oa_dec0, id_fd1, id_dec0, cf_fd1, cf_dec0,
+                                                            weights=hw))
+                f = head_epilogue(fe1, oa_fd1, oa_dec0, id_fd1, id_dec0, cf_fd1, cf_dec0, weights=hw)
+                ref = heads()
+            r["fused_max_abs_diff"] = max((a - b).abs().max().item() for a, b in zip(f, ref))
+            r["speedup_vs_torch"] = round(r["heads_total_ms"] / r["fused_ms"], 2)
+            # f32 matrix-core work actually issued: 32*MB rows x (2 sources x C x 9) per pixel
+            mb = (3 * args.K + 2 + 31) // 32
+            issued = B * H * W * 32 * mb * 2 * 64 * 9 + B * H * W * 2 * 64 * 9
+            r["fused_tflops_useful"] = round(2 * macs / (r["fused_ms"] * 1e-3) / 1e12, 2)
+            r["fused_tflops_issued"] = round(2 * issued / (r["fused_ms"] * 1e-3) / 1e12, 2)
+            r["fused_frac_f32_peak_issued"] = round(r["fused_tflops_issued"] / 157.3, 3)
+        except ImportError:
+            pass
         r["tflops_convs_only"] = round(2 * macs / ((r["conv_off_aff_ms"] + 2 * r["conv_1ch_ms"]) * 1e-3) / 1e12, 2)
         r["tflops_total"] = round(2 * macs / (r["heads_total_ms"] * 1e-3) / 1e12, 2)
         print(json.dumps(r), flush=True)
