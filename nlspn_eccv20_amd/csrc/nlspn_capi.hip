@@ -38,6 +38,9 @@ NLSPN_HD_EXTERN(1)
 NLSPN_HD_EXTERN(2)
 NLSPN_HD_EXTERN(3)
 NLSPN_HD_EXTERN(5)
+extern template __global__ void heads_kernel<1, true, 1>(HeadsArgs);
+extern template __global__ void heads_kernel<1, true, 2>(HeadsArgs);
+extern template __global__ void heads_kernel<1, true, 3>(HeadsArgs);
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -654,7 +657,8 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
     HeadsArgs a{static_cast<const float *>(fe1), static_cast<const float *>(fd_oa), static_cast<const float *>(fd_id),
                 static_cast<const float *>(fd_cf), wm, wv, bias, static_cast<float *>(off_aff),
                 static_cast<float *>(pred_init), static_cast<float *>(conf), B, C, H, W, nout,
-                (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH};
+                (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH, 0u};
+    if (const char *d = getenv("NLSPN_HEADS_DBG")) a.dbg = (unsigned)atoi(d);
     const long long grid = (long long)B * a.tiles_x * a.tiles_y;
     if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
     const bool vec = W % 4 == 0 && aligned(fe1, 16) && aligned(fd_oa, 16) && aligned(fd_id, 16) && aligned(fd_cf, 16);
@@ -665,7 +669,7 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
     case MB:                                                                                                \
         fn = vec ? reinterpret_cast<const void *>(&heads_kernel<MB, true>)                                  \
                  : reinterpret_cast<const void *>(&heads_kernel<MB, false>);                                \
-        lds = (int)sizeof(float) * HdCfg<MB>::LDS_FLOATS;                                                   \
+        lds = (int)sizeof(float) * (HdCfg<MB>::LDS_FLOATS + 2 * C * 9);                                     \
         break;
         NLSPN_HD_CASE(1)
         NLSPN_HD_CASE(2)
@@ -674,7 +678,22 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
 #undef NLSPN_HD_CASE
         default: return fail(NLSPN_EUNSUPPORTED, "head epilogue: nout=%d", nout);
     }
-    if (lds > 65536) NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    if (vec && head_mb(nout) == 1 && (a.dbg & 3u)) {  // ablation kernels (timing only)
+        const void *abl[3] = {reinterpret_cast<const void *>(&heads_kernel<1, true, 1>),
+                              reinterpret_cast<const void *>(&heads_kernel<1, true, 2>),
+                              reinterpret_cast<const void *>(&heads_kernel<1, true, 3>)};
+        fn = abl[(a.dbg & 3u) - 1];
+    }
+    if (lds > 65536) {  // once per kernel and size (idempotent, so an unlocked check is harmless)
+        static const void *set_fn[16];
+        static int set_lds[16];
+        int k = 0;
+        while (k < 16 && set_fn[k] && !(set_fn[k] == fn && set_lds[k] >= lds)) ++k;
+        if (k == 16 || !set_fn[k]) {
+            NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            if (k < 16) { set_lds[k] = lds; set_fn[k] = fn; }
+        }
+    }
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kHdNT), args, (size_t)lds, as_stream(stream)));
     return check_launch("nlspn_head_epilogue");

@@ -14,14 +14,17 @@
 //     id conv, nout+1 the cf conv, the rest zero), N = 32 pixels of one tile row,
 //     k over fe1 (all columns) and over off_aff_fd1 (off_aff columns only);
 //   * VALU part: the 1-channel id / cf convs' own decoder halves (id_fd1, cf_fd1),
-//     one pixel per thread, weights from scalar registers (wave-uniform loads).
-//     As MFMA columns they would cost 32x their FLOPs.
-// Tile: 8 rows x 32 columns, 256 threads (4 waves, 2 rows each).  The K loop runs
-// over 16-channel chunks: the chunk's input window (16 ch x 10 rows x 40 cols, zero
+//     one pixel per thread, weights from scalar registers (wave-uniform loads), issued
+//     in the same loop body as the MFMAs (the matrix cores' shadow).  As MFMA columns
+//     they would cost 32x their FLOPs.
+// Tile: 8 rows x 32 columns, 256 threads (4 waves, 2 rows each).  The K loop runs in
+// rounds of 16 channels: the round's two input windows (16 ch x 10 rows x 40 cols, zero
 // outside the image = the conv's zero padding) and its packed weights are staged in
-// LDS; the next chunk's global loads are in flight in registers while the current
-// chunk computes.
+// LDS; the next round's global loads are in flight in registers while the current
+// round computes.  LDS 74 KB and 239 registers: two workgroups per CU.
 #pragma once
+
+#include <type_traits>
 
 #include "nlspn_common.h"
 
@@ -43,6 +46,8 @@ struct HeadsArgs {
     float *pred_init;   // (B,1,H,W) or null
     float *conf;        // (B,1,H,W) or null
     int B, C, H, W, nout, tiles_x, tiles_y;
+    unsigned dbg;  // NLSPN_HEADS_DBG (ablation, timing only): 1 no VALU sums, 2 no MFMAs (both: the ABL
+                   // kernels of MB=1), 4 no LDS staging
 };
 
 template <int MB> struct HdCfg {
@@ -50,21 +55,73 @@ template <int MB> struct HdCfg {
     static constexpr int WCS = 9 * NCO + ((MB % 2) ? 0 : 32);  // LDS weight channel stride: 32 (mod 64) banks
     static constexpr int WF4 = kHdCC * 9 * NCO / 4;              // float4s of one chunk's weights
     static constexpr int WR = (WF4 + kHdNT - 1) / kHdNT;
-    static constexpr int LDS_FLOATS = kHdCC * kHdCS + kHdCC * WCS + 2 * kHdTH * kHdTW;
+    static constexpr int LDS_FLOATS = 2 * kHdCC * kHdCS + kHdCC * WCS + 2 * kHdTH * kHdTW;  // + 2*C*9 (VALU weights)
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// Chunk q: q < 2*NCH are MFMA chunks (source q / NCH: fe1, off_aff_fd1), then the VALU
-// chunks of id_fd1 and cf_fd1 (those present).
-template <int MB, bool VEC>
-__global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
+// One input window of a chunk (16 channels x 10 rows x 40 columns) in flight in
+// registers: raw bits + a per-float4 in-image mask.  Every lane loads a clamped,
+// in-bounds address and the mask zeroes what lies outside the image when the window is
+// written to LDS: a select right after the load would let the compiler sink the load
+// into a branch and wait for it at the join (one full memory latency per load).
+template <bool VEC> struct HdWin {
+    u32x4 r[kHdXR];  // ext-vector types: a HIP float4 struct copy from global memory becomes
+    unsigned m[kHdXR];  // a memcpy that keeps the array in scratch
+
+    __device__ __forceinline__ void load(const float *src, long long HW, int H, int W, int y0, int x0, int tid) {
+#pragma unroll
+        for (int i = 0; i < kHdXR; ++i) {
+            const int f = min(tid + i * kHdNT, kHdXF4 - 1);
+            const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
+            const int row = rem / (kHdRS / 4), c4 = rem - row * (kHdRS / 4);
+            const int y = y0 - 1 + row, x = x0 - 4 + 4 * c4;
+            const bool yin = (unsigned)y < (unsigned)H;
+            const float *p = src + ch * HW + (long long)min(max(y, 0), H - 1) * W;
+            if (VEC) {
+                r[i] = *reinterpret_cast<const u32x4 *>(p + min(max(x, 0), W - 4));
+                m[i] = (yin && (unsigned)x < (unsigned)W) ? 0xfu : 0u;
+            } else {
+                unsigned mm = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    r[i][j] = __builtin_bit_cast(unsigned, p[min(max(x + j, 0), W - 1)]);
+                    mm |= (yin && (unsigned)(x + j) < (unsigned)W) ? (1u << j) : 0u;
+                }
+                m[i] = mm;
+            }
+        }
+    }
+    __device__ __forceinline__ void store(float *XL, int tid) const {
+#pragma unroll
+        for (int i = 0; i < kHdXR; ++i) {
+            const int f = tid + i * kHdNT;
+            if (f < kHdXF4) {
+                const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
+                const u32x4 mk = {(m[i] & 1u) ? ~0u : 0u, (m[i] & 2u) ? ~0u : 0u, (m[i] & 4u) ? ~0u : 0u,
+                                  (m[i] & 8u) ? ~0u : 0u};
+                *reinterpret_cast<u32x4 *>(&XL[ch * kHdCS + 4 * rem]) = r[i] & mk;  // rows of 40 = 10 float4
+            }
+        }
+    }
+};
+
+// Round r (0 .. 2*C/16-1) stages three chunks of 16 channels: the MFMA source (fe1 for
+// r < C/16, then off_aff_fd1), its packed weights, and the VALU source (id_fd1 for
+// r < C/16, then cf_fd1).  The VALU sums (18 FMAs per channel pair) sit in the same loop
+// body as the channel pair's 18 MFMAs, so they issue in the matrix cores' shadow.  An
+// absent id / cf source is replaced by fe1 (valid memory) and its sum discarded: every
+// round runs the same straight-line code.
+template <int MB, bool VEC, int ABL = 0>
+__global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2))) heads_kernel(HeadsArgs a) {
     using Cfg = HdCfg<MB>;
     constexpr int NCO = Cfg::NCO, WCS = Cfg::WCS;
     extern __shared__ float hd_lds[];
-    float *XL = hd_lds;                       // [16][CS]
-    float *WL = XL + kHdCC * kHdCS;           // [16][WCS]
-    float *SV = WL + kHdCC * WCS;             // [2][256]: the VALU sums per pixel
+    float *XL = hd_lds;                       // [16][CS]   MFMA source window
+    float *XV = XL + kHdCC * kHdCS;           // [16][CS]   VALU source window
+    float *WL = XV + kHdCC * kHdCS;           // [16][WCS]  packed weights
+    float *SV = WL + kHdCC * WCS;             // [2][256]   the VALU sums per pixel
+    float *WVL = SV + 2 * kHdNT;              // [2][C][9]  the VALU weights (all rounds)
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int ntile = a.tiles_x * a.tiles_y * a.B;
@@ -74,79 +131,19 @@ __global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
     const int y0 = ty * kHdTH, x0 = tx * kHdTW;
     const int H = a.H, W = a.W, C = a.C;
     const long long HW = (long long)H * W;
-    const int nch = C / kHdCC;
-    const int nmfma = 2 * nch;
-    const int nvalu = ((a.fd_id != nullptr) + (a.fd_cf != nullptr)) * nch;
-    const int nq = nmfma + nvalu;
+    const int nch = C / kHdCC, nr = 2 * nch;
+    const float *vsrc[2] = {a.fd_id ? a.fd_id : a.fe1, a.fd_cf ? a.fd_cf : a.fe1};
 
-    auto source = [&](int q, int &cbase, int &vsrc) __attribute__((always_inline)) -> const float * {
-        if (q < nmfma) {
-            vsrc = -1;
-            cbase = (q % nch) * kHdCC;
-            return q < nch ? a.fe1 : a.fd_oa;
-        }
-        const int v = q - nmfma;
-        cbase = (v % nch) * kHdCC;
-        const bool id_first = a.fd_id != nullptr;
-        vsrc = (v < nch && id_first) ? 0 : 1;
-        return vsrc == 0 ? a.fd_id : a.fd_cf;
-    };
-
-    f32x4 xr[kHdXR];  // ext-vector type: a HIP float4 struct copy from global memory
-    f32x4 wr[Cfg::WR];  // becomes a memcpy that keeps the array in scratch
-    auto load_chunk = [&](int q) __attribute__((always_inline)) {
-        int cbase, vsrc;
-        const float *src = source(q, cbase, vsrc) + ((long long)b * C + cbase) * HW;
-#pragma unroll
-        for (int i = 0; i < kHdXR; ++i) {
-            // every lane loads (clamped, in-bounds address) and zeroes what lies outside
-            // the image afterwards: no divergent branches around the loads, so they stay
-            // in registers and all go out back to back
-            const int f = min(tid + i * kHdNT, kHdXF4 - 1);
-            const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
-            const int row = rem / (kHdRS / 4), c4 = rem - row * (kHdRS / 4);
-            const int y = y0 - 1 + row, x = x0 - 4 + 4 * c4;
-            const bool yin = (unsigned)y < (unsigned)H;
-            const float *p = src + ch * HW + (long long)min(max(y, 0), H - 1) * W;
-            f32x4 v;
-            if (VEC) {
-                v = *reinterpret_cast<const f32x4 *>(p + min(max(x, 0), W - 4));
-                if (!yin || (unsigned)x >= (unsigned)W) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-                float e[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    e[j] = p[min(max(x + j, 0), W - 1)];
-                    if (!yin || (unsigned)(x + j) >= (unsigned)W) e[j] = 0.f;
-                }
-                v = f32x4{e[0], e[1], e[2], e[3]};
-            }
-            xr[i] = v;
-        }
-        // weights: loaded (and staged) for VALU chunks too — a redundant copy of a valid
-        // chunk — so that wr is assigned on every path and stays in registers
-        const int wq = q < nmfma ? q : 0;
-        const f32x4 *wsrc = reinterpret_cast<const f32x4 *>(a.wm + ((long long)(wq / nch) * C + (wq % nch) * kHdCC) * 9 * NCO);
+    HdWin<VEC> xm, xv;
+    f32x4 wr[Cfg::WR];
+    auto load_round = [&](int r) __attribute__((always_inline)) {
+        const int s = r < nch ? 0 : 1, cb = (r - s * nch) * kHdCC;
+        const long long off = ((long long)b * C + cb) * HW;
+        xm.load((s == 0 ? a.fe1 : a.fd_oa) + off, HW, H, W, y0, x0, tid);
+        xv.load(vsrc[s] + off, HW, H, W, y0, x0, tid);
+        const f32x4 *wsrc = reinterpret_cast<const f32x4 *>(a.wm + ((long long)s * C + cb) * 9 * NCO);
 #pragma unroll
         for (int i = 0; i < Cfg::WR; ++i) wr[i] = wsrc[min(tid + i * kHdNT, Cfg::WF4 - 1)];
-    };
-    auto store_chunk = [&](int q) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < kHdXR; ++i) {
-            const int f = tid + i * kHdNT;
-            if (f < kHdXF4) {
-                const int ch = f / ((kHdTH + 2) * (kHdRS / 4)), rem = f - ch * ((kHdTH + 2) * (kHdRS / 4));
-                *reinterpret_cast<f32x4 *>(&XL[ch * kHdCS + 4 * rem]) = xr[i];  // rows of 40 = 10 float4
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < Cfg::WR; ++i) {
-            const int f = tid + i * kHdNT;
-            if (f < Cfg::WF4) {
-                const int ch = f / (9 * NCO / 4), rem = f - ch * (9 * NCO / 4);
-                *reinterpret_cast<f32x4 *>(&WL[ch * WCS + 4 * rem]) = wr[i];
-            }
-        }
     };
 
     f32x16 acc[MB][2];
@@ -159,45 +156,69 @@ __global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
     float sv_id = 0.f, sv_cf = 0.f;  // VALU sums of this thread's pixel
     const int vrow = tid >> 5, vcol = tid & 31;
 
-    load_chunk(0);
-    for (int q = 0; q < nq; ++q) {
-        __syncthreads();  // the previous chunk's LDS reads are done
-        store_chunk(q);
+    for (int i = tid; i < 2 * C * 9; i += kHdNT) WVL[i] = a.wv[i];  // read as LDS broadcasts
+    load_round(0);
+    for (int r = 0; r < nr; ++r) {
+        __syncthreads();  // the previous round's LDS reads are done
+        if (!(a.dbg & 4u)) {
+            xm.store(XL, tid);
+            xv.store(XV, tid);
+#pragma unroll
+            for (int i = 0; i < Cfg::WR; ++i) {
+                const int f = tid + i * kHdNT;
+                if (f < Cfg::WF4) {
+                    const int ch = f / (9 * NCO / 4), rem = f - ch * (9 * NCO / 4);
+                    *reinterpret_cast<f32x4 *>(&WL[ch * WCS + 4 * rem]) = wr[i];
+                }
+            }
+        }
         __syncthreads();
-        if (q + 1 < nq) load_chunk(q + 1);  // in flight while this chunk computes
-        if (q < nmfma) {
-            // B operand: X[k = h][px = l32] of channel 2cp+h at tap (dy,dx), rows 2wv+n
-            const float *xb = XL + h * kHdCS + (2 * wv) * kHdRS + l32 + 3;
-            const float *wb = WL + h * WCS + l32;
+        // the next round's loads, in flight while this round computes (the last round
+        // reloads round 0, unused: no branch, so no wait at a join)
+        load_round(r + 1 < nr ? r + 1 : 0);
+        const int s = r < nch ? 0 : 1;
+        const float *wvp = WVL + (s * C + (r - s * nch) * kHdCC) * 9;  // same address in every lane: broadcasts
+        // B operand: X[k = h][px = l32] of channel 2cp+h at tap (dy,dx), rows 2wv+n;
+        // A operand: W[co = 32m + l32][k = h] of the same channel and tap
+        const float *xb = XL + h * kHdCS + (2 * wv) * kHdRS + l32 + 3;
+        const float *wb = WL + h * WCS + l32;
+        const float *xvp = XV + vrow * kHdRS + vcol + 3;
+        // the round's straight-line body; the ablation variants (ABL = NLSPN_HEADS_DBG & 3)
+        // are separate kernels, so no branch sits inside the MFMA stream
+        auto body = [&](auto do_mfma, auto do_valu) __attribute__((always_inline)) {
+            float sacc = 0.f;
 #pragma unroll
             for (int cp = 0; cp < kHdCC / 2; ++cp) {
 #pragma unroll
                 for (int t = 0; t < 9; ++t) {
                     const int dy = t / 3, dx = t % 3;
-                    float av[MB], bv[2];
+                    if constexpr (decltype(do_mfma)::value) {
+                        float av[MB], bv[2];
 #pragma unroll
-                    for (int m = 0; m < MB; ++m) av[m] = wb[2 * cp * WCS + t * NCO + 32 * m];
+                        for (int m = 0; m < MB; ++m) av[m] = wb[2 * cp * WCS + t * NCO + 32 * m];
 #pragma unroll
-                    for (int n = 0; n < 2; ++n) bv[n] = xb[2 * cp * kHdCS + (n + dy) * kHdRS + dx];
+                        for (int n = 0; n < 2; ++n) bv[n] = xb[2 * cp * kHdCS + (n + dy) * kHdRS + dx];
 #pragma unroll
-                    for (int m = 0; m < MB; ++m)
+                        for (int m = 0; m < MB; ++m)
 #pragma unroll
-                        for (int n = 0; n < 2; ++n)
-                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+                            for (int n = 0; n < 2; ++n)
+                                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+                    }
+                    if constexpr (decltype(do_valu)::value) {
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int ch = 2 * cp + e;
+                            sacc += xvp[ch * kHdCS + dy * kHdRS + dx] * wvp[ch * 9 + t];
+                        }
+                    }
                 }
             }
-        } else {
-            int cbase, vsrc;
-            source(q, cbase, vsrc);
-            const float *wvp = a.wv + ((long long)vsrc * C + cbase) * 9;  // wave-uniform: scalar loads
-            const float *xv = XL + vrow * kHdRS + vcol + 3;
-            float s = 0.f;
-#pragma unroll
-            for (int ch = 0; ch < kHdCC; ++ch)
-#pragma unroll
-                for (int t = 0; t < 9; ++t) s += xv[ch * kHdCS + (t / 3) * kHdRS + (t % 3)] * wvp[ch * 9 + t];
-            if (vsrc == 0) sv_id += s; else sv_cf += s;
-        }
+            return sacc;
+        };
+        float svr;
+        svr = body(std::integral_constant<bool, !(ABL & 2)>{}, std::integral_constant<bool, !(ABL & 1)>{});
+        sv_id += s == 0 ? svr : 0.f;
+        sv_cf += s == 1 ? svr : 0.f;
     }
 
     // epilogue: the VALU sums by pixel, then bias + activation and coalesced row stores
@@ -205,6 +226,11 @@ __global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
     SV[kHdNT + tid] = sv_cf;
     __syncthreads();
     const int x = x0 + l32;
+    float bv[MB][16];  // biases of this lane's 16*MB output channels, all loads issued together
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[m][r] = a.bias[32 * m + (r & 3) + 8 * (r >> 2) + 4 * h];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         const int yl = 2 * wv + n, y = y0 + yl;
@@ -215,7 +241,7 @@ __global__ void __launch_bounds__(kHdNT) heads_kernel(HeadsArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int co = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float v = acc[m][n][r] + a.bias[co];
+                const float v = acc[m][n][r] + bv[m][r];
                 if (co < a.nout) {
                     a.off_aff[((long long)b * a.nout + co) * HW + pix] = v;
                 } else if (co == a.nout) {

@@ -12,4 +12,8 @@ NLSPN_HD_INST(1)
 NLSPN_HD_INST(2)
 NLSPN_HD_INST(3)
 NLSPN_HD_INST(5)
+// ablation variants (NLSPN_HEADS_DBG bits 1, 2; tools/head_ablate.py)
+template __global__ void heads_kernel<1, true, 1>(HeadsArgs);
+template __global__ void heads_kernel<1, true, 2>(HeadsArgs);
+template __global__ void heads_kernel<1, true, 3>(HeadsArgs);
 }  // namespace nlspn
