@@ -176,6 +176,7 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
         // the next round's loads, in flight while this round computes (the last round
         // reloads round 0, unused: no branch, so no wait at a join)
         load_round(r + 1 < nr ? r + 1 : 0);
+        __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the compute (the scheduler sinks them otherwise)
         const int s = r < nch ? 0 : 1;
         const float *wvp = WVL + (s * C + (r - s * nch) * kHdCC) * 9;  // same address in every lane: broadcasts
         // B operand: X[k = h][px = l32] of channel 2cp+h at tap (dy,dx), rows 2wv+n;
@@ -186,34 +187,49 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
         // the round's straight-line body; the ablation variants (ABL = NLSPN_HEADS_DBG & 3)
         // are separate kernels, so no branch sits inside the MFMA stream
         auto body = [&](auto do_mfma, auto do_valu) __attribute__((always_inline)) {
-            float sacc = 0.f;
+            // software pipelined by hand: the LDS operands of k-step j+1 are read while
+            // the MFMAs of step j issue; scheduling barriers keep the compiler from
+            // sinking the reads next to their use (it does, to save registers, and then
+            // every MFMA waits on an LDS round trip)
+            constexpr int NS = (kHdCC / 2) * 9;  // k-steps (channel pair, tap) per round
+            float av[2][MB], bv[2][2], xv[2][2], wv2[2][2];
+            auto fetch = [&](int j, int slot) __attribute__((always_inline)) {
+                const int cp = j / 9, t = j % 9, dy = t / 3, dx = t % 3;
+                if constexpr (decltype(do_mfma)::value) {
 #pragma unroll
-            for (int cp = 0; cp < kHdCC / 2; ++cp) {
+                    for (int m = 0; m < MB; ++m) av[slot][m] = wb[2 * cp * WCS + t * NCO + 32 * m];
 #pragma unroll
-                for (int t = 0; t < 9; ++t) {
-                    const int dy = t / 3, dx = t % 3;
-                    if constexpr (decltype(do_mfma)::value) {
-                        float av[MB], bv[2];
+                    for (int n = 0; n < 2; ++n) bv[slot][n] = xb[2 * cp * kHdCS + (n + dy) * kHdRS + dx];
+                }
+                if constexpr (decltype(do_valu)::value) {
 #pragma unroll
-                        for (int m = 0; m < MB; ++m) av[m] = wb[2 * cp * WCS + t * NCO + 32 * m];
-#pragma unroll
-                        for (int n = 0; n < 2; ++n) bv[n] = xb[2 * cp * kHdCS + (n + dy) * kHdRS + dx];
-#pragma unroll
-                        for (int m = 0; m < MB; ++m)
-#pragma unroll
-                            for (int n = 0; n < 2; ++n)
-                                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-                    }
-                    if constexpr (decltype(do_valu)::value) {
-#pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            const int ch = 2 * cp + e;
-                            sacc += xvp[ch * kHdCS + dy * kHdRS + dx] * wvp[ch * 9 + t];
-                        }
+                    for (int e = 0; e < 2; ++e) {
+                        xv[slot][e] = xvp[(2 * cp + e) * kHdCS + dy * kHdRS + dx];
+                        wv2[slot][e] = wvp[(2 * cp + e) * 9 + t];
                     }
                 }
+            };
+            float sacc[2] = {0.f, 0.f};
+            fetch(0, 0);
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const int cur = j & 1;
+                if (j + 1 < NS) fetch(j + 1, cur ^ 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (decltype(do_mfma)::value) {
+#pragma unroll
+                    for (int m = 0; m < MB; ++m)
+#pragma unroll
+                        for (int n = 0; n < 2; ++n)
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][m], bv[cur][n], acc[m][n], 0, 0, 0);
+                }
+                if constexpr (decltype(do_valu)::value) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) sacc[e] += xv[cur][e] * wv2[cur][e];
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
-            return sacc;
+            return sacc[0] + sacc[1];
         };
         float svr;
         svr = body(std::integral_constant<bool, !(ABL & 2)>{}, std::integral_constant<bool, !(ABL & 1)>{});
