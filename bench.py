@@ -42,6 +42,7 @@ per-iteration step kernel):
       FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes), or null.
 Extra objects (headline config only, not part of `value`): backward (fp32
 forward+backward through autograd), gru_section (the reference's default GRU mode),
+head_epilogue (the decoder's last three convs fused into one HIP kernel vs torch.cat + MIOpen),
 cpu_baseline (rank 0, N=1; the C oracle for the offset path and the reference's
 own torch op sequence for the no-offset path, all threads and 1 thread).
 """
@@ -98,6 +99,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-backward", action="store_true")
+    ap.add_argument("--no-heads", action="store_true", help="skip the head-epilogue (fused conv) leg")
     ap.add_argument("--no-gru", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true")
     ap.add_argument("--backward-steps", type=int, default=20)
@@ -329,6 +331,61 @@ def gru_section_timing(inputs, cfg, steps, dev):
             "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration"}
 
 
+def head_epilogue_timing(cfg, dev, reps=20):
+    """The head epilogue (nlspnmodel.py:296-315): the decoder's last
+    three 3x3 convs (off_aff_dec0 -> 3K, id_dec0 -> 1 + ReLU, cf_dec0 -> 1 + Sigmoid) on
+    fe1 and the three 64-channel decoder outputs, at this config's B x H x W, fused HIP
+    kernel (nlspn_head_epilogue) vs the reference's op sequence on torch (torch.cat +
+    MIOpen conv + activation).  Synthetic U(0,1) activations, default-init weights; CUDA
+    events, median of `reps` after 5 warm-ups.  Not part of `value`."""
+    import torch.nn as nn
+    from nlspn_eccv20_amd.heads import HeadWeights, head_epilogue
+    B, H, W = cfg["B"], cfg["H"], cfg["W"]
+    K = cfg["kernel"][0] * cfg["kernel"][1] - 1
+    g = torch.Generator(device=dev).manual_seed(11)
+    fe1, id_fd1, oa_fd1, cf_fd1 = (torch.rand((B, 64, H, W), device=dev, generator=g) for _ in range(4))
+    torch.manual_seed(11)
+    oa, idc, cfc = (nn.Conv2d(128, n, 3, padding=1).to(dev) for n in (3 * K, 1, 1))
+    hw = HeadWeights()
+
+    def fused():
+        return head_epilogue(fe1, oa_fd1, oa, id_fd1, idc, cf_fd1, cfc, weights=hw)
+
+    def ref():
+        return (torch.relu(idc(torch.cat((id_fd1, fe1), 1))), oa(torch.cat((oa_fd1, fe1), 1)),
+                torch.sigmoid(cfc(torch.cat((cf_fd1, fe1), 1))))
+
+    def med(fn):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return statistics.median(ts)
+
+    with torch.no_grad():
+        t_fused, t_ref = med(fused), med(ref)
+        f, r = fused(), ref()
+        diff = max((a - b).abs().max().item() for a, b in zip(f, r))
+    del fe1, id_fd1, oa_fd1, cf_fd1
+    flops = 2.0 * B * H * W * 128 * 9 * (3 * K + 2)
+    ach = flops / (t_fused * 1e-3) / 1e12
+    return {"ms_fused": round(t_fused, 4), "ms_torch": round(t_ref, 4), "speedup": round(t_ref / t_fused, 2),
+            "max_abs_diff_vs_torch": diff,
+            "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
+                         "frac": round(ach / 157.3, 3),
+                         "basis": "useful FLOPs 2*B*H*W*128*9*(3K+2) / fused-call time; peak = f32-input MFMA "
+                                  "(v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md)"},
+            "note": "fused: one HIP kernel (nlspn_heads.h, f32 operands on the matrix cores), reads fe1 + decoder "
+                    "outputs in place; torch: 3 x (torch.cat + MIOpen conv) + ReLU/Sigmoid"}
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -450,6 +507,9 @@ def main():
     if cfg["dtype"] == "f32" and cfg["kernel"] == (3, 3) and not a.no_gru:
         out["gru_section"] = gru_section_timing(inputs, cfg, a.backward_steps, dev)
     del inputs
+    if cfg["dtype"] == "f32" and not a.no_heads:
+        out["head_epilogue"] = head_epilogue_timing(cfg, dev)
+        torch.cuda.empty_cache()
     if not a.no_extra_configs:
         out["configs"] = {}
         for name in EXTRA:

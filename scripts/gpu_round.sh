@@ -24,7 +24,7 @@ for CFG in nyu kitti nyu_k16; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_${CFG}_$C -o run --output-format csv -- \
         python3 $R/bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-backward --no-gru \
-        --no-extra-configs --kernel-reps 5 > $O/pmc_${CFG}_$C.log 2>&1 || exit 1
+        --no-extra-configs --no-heads --kernel-reps 5 > $O/pmc_${CFG}_$C.log 2>&1 || exit 1
   done
   python3 $R/tools/pmc_summary.py --bench $CFG "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over bench.py --config $CFG (scripts/gpu_round.sh $TAG)" \
       $O/pmc_$CFG.json $O/pmc_${CFG}_FETCH_SIZE/run_counter_collection.csv $O/pmc_${CFG}_WRITE_SIZE/run_counter_collection.csv \
