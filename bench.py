@@ -326,9 +326,31 @@ def gru_section_timing(inputs, cfg, steps, dev):
         e[3].record()
     torch.cuda.synchronize()
     eager, graph = e[0].elapsed_time(e[1]) / steps, e[2].elapsed_time(e[3]) / steps
+    del g
+    # the same section with the GRU convolutions in channels_last and MIOpen's algorithm
+    # search on (NLSPNModel.gru_channels_last; cudnn.benchmark restored afterwards)
+    prev = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = True
+    try:
+        m.gru_channels_last()
+        g = SectionGraph(m, *heads)
+        with torch.no_grad():
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+            e[0].record()
+            for _ in range(steps):
+                g.replay()
+            e[1].record()
+        torch.cuda.synchronize()
+        tuned = e[0].elapsed_time(e[1]) / steps
+    finally:
+        torch.backends.cudnn.benchmark = prev
     return {"ms_per_step_eager": round(eager, 4), "ms_per_step_graph": round(graph, 4),
-            "iters_per_s_graph": round(cfg["T"] / (graph * 1e-3), 1), "steps": steps,
-            "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration"}
+            "iters_per_s_graph": round(cfg["T"] / (graph * 1e-3), 1),
+            "ms_per_step_graph_channels_last_tuned": round(tuned, 4), "steps": steps,
+            "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration; "
+                    "tuned = GRU convs channels_last + MIOpen algorithm search"}
 
 
 def head_epilogue_timing(cfg, dev, reps=20):

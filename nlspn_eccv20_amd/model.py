@@ -249,6 +249,17 @@ class NLSPNModel(nn.Module):
         params = nn.ParameterList([p for p in self.parameters() if p.requires_grad])
         self.param_groups = [{"params": params, "lr": args.lr}]
 
+    def gru_channels_last(self):
+        """Put the GRU-mode convolutions (ConvGRU, encode_aff / encode_dep, decode_aff) in
+        channels_last: MIOpen's implicit-GEMM convolutions run NHWC, so this drops the
+        NCHW<->NHWC transposes around every one of them.  With MIOpen's algorithm search
+        (torch.backends.cudnn.benchmark) the GRU section at NYU B=8 goes 16.3 -> 11.2 ms
+        (tools/gru_prof.py).  Numerics: the same convolutions in another layout."""
+        if self.args.use_GRU:
+            for sub in (self.GRU, self.encode_aff, self.encode_dep, self.decode_aff):
+                sub.to(memory_format=torch.channels_last)
+        return self
+
     @staticmethod
     def _crop(fd, fe):
         """The decoder-padding crop of nlspnmodel.py:161-174."""

@@ -236,3 +236,21 @@ def test_section_graph_equals_eager(use_gru):
                 assert torch.equal(o["pred"], eager["pred"])
                 for a, b in zip(o["pred_inter"], eager["pred_inter"]):
                     assert torch.equal(a, b)
+
+
+def test_gru_channels_last_equals_default():
+    """gru_channels_last (the GRU-mode convolutions in NHWC) computes the same section:
+    the same convolutions in another layout (MIOpen may pick another algorithm, so f32
+    rounding differs; the propagated depth agrees to 1e-4 of its range)."""
+    torch.manual_seed(0)
+    m = NLSPNModel(make_args(prop_time=6, patch_height=48, patch_width=80)).to(DEV).eval()
+    randomize_aff_head(m)
+    s = sample(2, 48, 80, seed=5)
+    with torch.no_grad():
+        h = m.heads(s)
+        ref = m.propagate_heads(*h, s["dep"])
+        m.gru_channels_last()
+        got = m.propagate_heads(*h, s["dep"])
+    scale = ref["pred"].abs().max().item()
+    assert (got["pred"] - ref["pred"]).abs().max().item() <= 1e-4 * scale
+    assert (got["aff"] - ref["aff"]).abs().max().item() <= 1e-4
