@@ -209,4 +209,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return base + slot;
 }
 
+// Inverse of xcd_remap: the block index that xcd_remap maps to logical index L.
+__device__ __forceinline__ int xcd_unmap(int L, int nblk) {
+    const int q = nblk / kNumXcd, r = nblk % kNumXcd;
+    int xcd, slot;
+    if (L < r * (q + 1)) {
+        xcd = L / (q + 1);
+        slot = L - xcd * (q + 1);
+    } else {
+        const int L2 = L - r * (q + 1);
+        xcd = r + L2 / q;
+        slot = L2 - (xcd - r) * q;
+    }
+    return slot * kNumXcd + xcd;
+}
+
 }  // namespace nlspn

@@ -9,9 +9,9 @@
 // the register files and LDS (C2: all 8 NYU images, 60 MB; C3: 2 of the 4 KITTI
 // images) keeps them there:
 //
-//   * one workgroup per CU owns a RECTANGLE of pixel quads of one image (image
-//     b = blockIdx % B, part j = blockIdx / B = py * gx + px of a gy x gx grid of
-//     row bands x quad-column bands, so an image's parts share an XCD group); each
+//   * one workgroup per CU owns a RECTANGLE of pixel quads of one image (part
+//     j = py * gx + px of a gy x gx grid of row bands x quad-column bands; parts
+//     are dealt to XCDs in contiguous runs, so neighbouring parts share one); each
 //     thread owns one quad (4 pixels of a row) and holds its tap geometry and dep
 //     in VGPRs, its affinities and conf' in LDS, for the whole launch;
 //   * the part's f window — every cell any valid tap of the part reads (found once:
@@ -204,7 +204,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
 
     const int H = a.H, W = a.W, W4 = W / 4;
-    const int b = blockIdx.x % a.B, j = blockIdx.x / a.B;
+    // Part numbering: logical index L = b * (gy*gx) + j, dealt to the XCDs in contiguous
+    // runs (xcd_remap), so the parts of an image — and neighbouring parts — share an
+    // XCD where the counts allow (C2: one image per XCD; C3: each image over four XCDs
+    // in bands of 32 parts; C1: bands of 32 parts).  Speed only: progress words are
+    // indexed by blockIdx, and a consumer maps the parts it reads back (xcd_unmap).
+    const int nparts = a.gy * a.gx, G = a.B * nparts;
+    const int L = xcd_remap((int)blockIdx.x, G);
+    const int b = L / nparts, j = L - b * nparts;
     const int py = j / a.gx, px = j % a.gx;
     const int r0 = (int)((long long)py * H / a.gy), r1 = (int)((long long)(py + 1) * H / a.gy);    // own rows
     const int c0 = (int)((long long)px * W4 / a.gx), c1 = (int)((long long)(px + 1) * W4 / a.gx);  // own quad cols
@@ -417,7 +424,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- wait until every part this one reads has finished iteration t-1
         if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
-            bool fail = (a.dbg & 32u) && blockIdx.x == 0;  // test hook: part 0 of image 0 aborts
+            bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
             const unsigned need = a.epoch + (unsigned)(t - 1);
             for (int base = 0; base < ndep && !fail; base += 64) {
                 const int d = base + lane;
@@ -426,7 +433,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 for (;;) {
                     bool ok = true;
                     if (d < ndep)
-                        ok = __hip_atomic_load(&sync[1 + jj * a.B + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                        ok = __hip_atomic_load(&sync[1 + xcd_unmap(b * nparts + jj, G)], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) >=
                              need;
                     if (__all(ok)) break;
                     if (++spins > kResSpinLimit ||

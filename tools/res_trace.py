@@ -1,8 +1,9 @@
 """Critical-path trace of the resident kernel (NLSPN_RES_DBG=8): thread 0 of every part
 stamps s_memrealtime (100 MHz) at five points of each iteration — loop top (S0), after
 the wait barrier (S1), after staging (S2), before the drain (S3), after the publish
-barrier (S4) — into the `pred` buffer.  Prints per-phase medians (us) and the hand-off
-latency: a part's wait exit minus the latest publish of its neighbour parts."""
+barrier (S4) — into the `pred` buffer.  Prints per-phase medians (us) per image-group
+launch; "wait" is the hand-off latency plus the skew to the slowest neighbour part.
+usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1] [--bg IMAGES_PER_LAUNCH]"""
 import ctypes
 import json
 import os
@@ -17,9 +18,13 @@ from nlspn_eccv20_amd.propagation import _alloc_outputs, _propagate_args, _strea
 from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
 
 
-def main(B=8, H=228, W=304, T=18, reps=5):
+CONFIGS = {"nyu": (8, 228, 304, 500 / (228 * 304)), "kitti": (4, 240, 1216, 0.05), "nyu_b1": (1, 228, 304, 500 / (228 * 304))}
+
+
+def main(config="nyu", T=18, reps=5, bg=None):
+    B, H, W, density = CONFIGS[config]
     dev = torch.device("cuda", 0)
-    s = synth(B, H, W, 8, seed=7240, off_sigma=2.0, density=500 / (H * W))
+    s = synth(B, H, W, 8, seed=7240, off_sigma=2.0, density=density)
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
     oa = t(s["off_aff"])
     ins = (t(s["pred_init"]), t(s["dep"]), t(s["conf"]), oa[:, 16:], oa[:, :16], torch.tensor([4.0], device=dev))
@@ -27,7 +32,10 @@ def main(B=8, H=228, W=304, T=18, reps=5):
     grid = ctypes.c_int()
     os.environ["NLSPN_RESIDENT"] = "1"
     lib.nlspn_resident_config(0, B, H, W, 3, 3, T, 1, ctypes.byref(grid), None, None)
-    G, g = grid.value, grid.value // B
+    G = grid.value  # parts of one image-group launch
+    bg = bg or B    # images per launch (C3: 2)
+    ng = (B + bg - 1) // bg
+    g = G // bg
     os.environ["NLSPN_RES_DBG"] = "8"
     outs = _alloc_outputs(ins[0], 8, T, True, True)
     args, _ = _propagate_args(*ins, (3, 3), T, "TGASS", True, False, outs)
@@ -35,8 +43,17 @@ def main(B=8, H=228, W=304, T=18, reps=5):
         _lib.check(lib.nlspn_propagate(*args, _stream(dev)))
     torch.cuda.synchronize()
     os.environ.pop("NLSPN_RES_DBG")
-    st = outs["pred"].view(-1).view(torch.int64)[: G * T * 5].cpu().numpy().reshape(G, T, 5).astype(np.float64)
-    st = st / 100.0  # us
+    HW = H * W
+    allst = outs["pred"].view(-1).view(torch.int64).cpu().numpy()
+    res = {}
+    for grp in range(ng):
+        o = grp * bg * HW // 2  # group k's stamps start at its own pred planes (int64 = 2 floats)
+        st = allst[o: o + G * T * 5].reshape(G, T, 5).astype(np.float64) / 100.0  # us
+        res[f"group{grp}"] = phases(st, G, B if ng == 1 else bg, g, T)
+    print(json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res}))
+
+
+def phases(st, G, B, g, T):
     st -= st[:, 0, 0].min()  # row t = 0: setup stamps (entry, invariants loaded, window zeroed, taps classified)
     su = st[:, 0, :]
     setup = {"entry_spread": su[:, 0].max() - su[:, 0].min(), "invariant_loads": np.median(su[:, 1] - su[:, 0]),
@@ -48,20 +65,17 @@ def main(B=8, H=228, W=304, T=18, reps=5):
     ph["loop"] = st[:, 1:, 0] - st[:, :-1, 4]
     out = {k: {"median": round(float(np.median(v)), 3), "p90": round(float(np.percentile(v, 90)), 3)}
            for k, v in ph.items()}
-    # hand-off latency: wait exit of part (j, b) at iteration t vs the latest publish of parts j-1..j+1 at t-1
-    lat = []
-    for blk in range(G):
-        b, j = blk % B, blk // B
-        nb = [jj * B + b for jj in (j - 1, j, j + 1) if 0 <= jj < g]
-        for it in range(1, st.shape[1]):
-            lat.append(st[blk, it, 1] - max(st[n, it - 1, 4] for n in nb))
-    out["publish_to_wait_exit"] = {"median": round(float(np.median(lat)), 3), "p90": round(float(np.percentile(lat, 90)), 3)}
     span = st[:, -1, 4].max() - st[:, 0, 0].min()
     out["span_us"] = round(float(span), 2)
     out["per_iter_us"] = round(float(span) / st.shape[1], 3)
     out["setup"] = {k: round(float(v), 3) for k, v in setup.items()}
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="nyu", choices=sorted(CONFIGS))
+    ap.add_argument("--bg", type=int, default=None, help="images per resident launch (C3: 2)")
+    a = ap.parse_args()
+    main(a.config, bg=a.bg)
