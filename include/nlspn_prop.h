@@ -106,6 +106,24 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
                         int B, int C, int H, int W, int nout, void *stream);
 
 /*
+ * The head epilogue with the propagation prologue fused in (3x3, K = 8, offsets on):
+ * instead of the raw off_aff planes the epilogue writes what step 1 of the section
+ * would — off_out = _off_insert(off) (nlspnmodel.py:324, B x 18 x H x W), aff_out =
+ * _affinity_normalization + _aff_insert (:325, B x 9 x H x W), conf_out = the blended
+ * confidence (:328-334, NULL with fd_cf), pred_init (:297) and p0 = the blended
+ * [clamped] pred_init that iteration 1 propagates (:341-348) — then
+ * nlspn_propagate_normalized runs the T iterations from them.  Same IEEE sequence as
+ * nlspn_propagate's step 1: bit-identical outputs given the same convolution sums.
+ * gamma: device pointer (learnable aff_scale_const); kind: NLSPN_AFF_*.
+ */
+int nlspn_head_epilogue_prologue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id,
+                                 const void *fd_cf, const float *wm, const float *wv,
+                                 const float *bias, const void *dep, const float *gamma,
+                                 void *pred_init, void *conf_out, void *aff_out, void *off_out,
+                                 void *p0, int B, int C, int H, int W, int kh, int kw, int kind,
+                                 unsigned flags, void *stream);
+
+/*
  * Affinity normalisation + reference-tap insertion.
  * Replaces NLSPNModel._affinity_normalization (src/model/nlspnmodel.py:179-201)
  * followed by _aff_insert (:261-269).
@@ -317,6 +335,20 @@ int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, cons
                          void *aff_out, void *off_out, void *conf_out, void *workspace,
                          int B, int H, int W, int kh, int kw, int T, int kind, unsigned flags,
                          int reps, void *stream, float *first_ms, float *rest_ms, int *resident);
+
+/*
+ * The propagation loop (nlspnmodel.py:340-381) from already-prologued inputs: p0
+ * (iteration 1's input), conf_eff (the blended confidence, or NULL), aff_norm
+ * (B x (K+1) planes, normalised, reference tap inserted), off_ins (B x 2(K+1)
+ * planes, _off_insert layout) — the outputs of nlspn_head_epilogue_prologue or of
+ * nlspn_propagate's step 1.  Writes pred_inter (T x B planes) and pred as
+ * nlspn_propagate does (same kernels: iteration 1 a plain step, 2..T resident where it
+ * applies); workspace as nlspn_propagate's.
+ */
+int nlspn_propagate_normalized(int dtype, const void *p0, const void *dep, const void *conf_eff,
+                               const void *aff_norm, const void *off_ins, void *pred_inter,
+                               void *pred, void *workspace, int B, int H, int W, int kh,
+                               int kw, int T, unsigned flags, void *stream);
 
 /*
  * Diagnostics: 1 if nlspn_propagate would run iterations 2..T as the resident

@@ -36,6 +36,9 @@ SIGNATURES = {
     "nlspn_head_packed_size": (_i, [_i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "nlspn_head_pack_weights": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "nlspn_head_epilogue": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nlspn_head_epilogue_prologue": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _i, _i, _i, _i, _i, _i, _i, _u, _vp]),
+    "nlspn_propagate_normalized": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _u, _vp]),
     "nlspn_prop_step": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i, _vp, _vp, _i, _i, _i, _i, _i, _u, _vp]),
     "nlspn_workspace_bytes": (_sz, [_i, _i, _i, _i]),
     "nlspn_propagate": (_i, [_i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -645,23 +645,13 @@ int nlspn_head_pack_weights(const float *w_oa, const float *b_oa, const float *w
     return check_launch("nlspn_head_pack_weights");
 }
 
-int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id, const void *fd_cf,
-                        const float *wm, const float *wv, const float *bias, void *off_aff, void *pred_init,
-                        void *conf, int B, int C, int H, int W, int nout, void *stream) {
-    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "head epilogue: float32 only (dtype %d)", dtype);
-    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
-    if (int rc = nlspn_head_packed_size(C, nout, nullptr, nullptr, nullptr)) return rc;
-    if (!fe1 || !fd_oa || !wm || !wv || !bias || !off_aff) return fail(NLSPN_EINVAL, "head epilogue: null pointer");
-    if ((fd_id == nullptr) != (pred_init == nullptr) || (fd_cf == nullptr) != (conf == nullptr))
-        return fail(NLSPN_EINVAL, "head epilogue: a head's source and output must both be given or both NULL");
-    HeadsArgs a{static_cast<const float *>(fe1), static_cast<const float *>(fd_oa), static_cast<const float *>(fd_id),
-                static_cast<const float *>(fd_cf), wm, wv, bias, static_cast<float *>(off_aff),
-                static_cast<float *>(pred_init), static_cast<float *>(conf), B, C, H, W, nout,
-                (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH, 0u};
-    if (const char *d = getenv("NLSPN_HEADS_DBG")) a.dbg = (unsigned)atoi(d);
+// Shared launch of both head-epilogue entry points.
+static int launch_heads(HeadsArgs &a, void *stream) {
+    const int B = a.B, C = a.C, H = a.H, W = a.W, nout = a.nout;
     const long long grid = (long long)B * a.tiles_x * a.tiles_y;
     if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
-    const bool vec = W % 4 == 0 && aligned(fe1, 16) && aligned(fd_oa, 16) && aligned(fd_id, 16) && aligned(fd_cf, 16);
+    const bool vec = W % 4 == 0 && aligned(a.fe1, 16) && aligned(a.fd_oa, 16) && aligned(a.fd_id, 16) &&
+                     aligned(a.fd_cf, 16);
     const void *fn = nullptr;
     int lds = 0;
     switch (head_mb(nout)) {
@@ -697,6 +687,89 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kHdNT), args, (size_t)lds, as_stream(stream)));
     return check_launch("nlspn_head_epilogue");
+}
+
+int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id, const void *fd_cf,
+                        const float *wm, const float *wv, const float *bias, void *off_aff, void *pred_init,
+                        void *conf, int B, int C, int H, int W, int nout, void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "head epilogue: float32 only (dtype %d)", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (int rc = nlspn_head_packed_size(C, nout, nullptr, nullptr, nullptr)) return rc;
+    if (!fe1 || !fd_oa || !wm || !wv || !bias || !off_aff) return fail(NLSPN_EINVAL, "head epilogue: null pointer");
+    if ((fd_id == nullptr) != (pred_init == nullptr) || (fd_cf == nullptr) != (conf == nullptr))
+        return fail(NLSPN_EINVAL, "head epilogue: a head's source and output must both be given or both NULL");
+    HeadsArgs a{static_cast<const float *>(fe1), static_cast<const float *>(fd_oa), static_cast<const float *>(fd_id),
+                static_cast<const float *>(fd_cf), wm, wv, bias, static_cast<float *>(off_aff),
+                static_cast<float *>(pred_init), static_cast<float *>(conf), B, C, H, W, nout,
+                (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                0u, 0u};
+    if (const char *d = getenv("NLSPN_HEADS_DBG")) a.dbg = (unsigned)atoi(d);
+    return launch_heads(a, stream);
+}
+
+int nlspn_head_epilogue_prologue(int dtype, const void *fe1, const void *fd_oa, const void *fd_id, const void *fd_cf,
+                                 const float *wm, const float *wv, const float *bias, const void *dep,
+                                 const float *gamma, void *pred_init, void *conf_out, void *aff_out, void *off_out,
+                                 void *p0, int B, int C, int H, int W, int kh, int kw, int kind, unsigned flags,
+                                 void *stream) {
+    if (dtype != NLSPN_DTYPE_F32) return fail(NLSPN_EUNSUPPORTED, "head epilogue: float32 only (dtype %d)", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (kh != 3 || kw != 3)
+        return fail(NLSPN_EUNSUPPORTED, "fused head prologue: 3x3 propagation only (k = %dx%d)", kh, kw);
+    if (kind < NLSPN_AFF_AS || kind > NLSPN_AFF_TGASS) return fail(NLSPN_EINVAL, "unknown affinity kind %d", kind);
+    const int nout = 3 * 8;
+    if (int rc = nlspn_head_packed_size(C, nout, nullptr, nullptr, nullptr)) return rc;
+    if (!fe1 || !fd_oa || !fd_id || !wm || !wv || !bias || !gamma || !pred_init || !aff_out || !off_out || !p0)
+        return fail(NLSPN_EINVAL, "fused head prologue: null pointer");
+    if ((fd_cf == nullptr) != (conf_out == nullptr))
+        return fail(NLSPN_EINVAL, "fused head prologue: cf_fd1 and conf_out must both be given or both NULL");
+    if ((flags & NLSPN_PRESERVE_INPUT) && !dep) return fail(NLSPN_EINVAL, "preserve_input requires dep");
+    HeadsArgs a{static_cast<const float *>(fe1), static_cast<const float *>(fd_oa), static_cast<const float *>(fd_id),
+                static_cast<const float *>(fd_cf), wm, wv, bias, nullptr, static_cast<float *>(pred_init),
+                static_cast<float *>(conf_out), B, C, H, W, nout, (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH,
+                static_cast<const float *>(dep), gamma, static_cast<float *>(aff_out), static_cast<float *>(off_out),
+                static_cast<float *>(p0), kind, flags, 0u};
+    return launch_heads(a, stream);
+}
+
+int nlspn_propagate_normalized(int dtype, const void *p0, const void *dep, const void *conf_eff,
+                               const void *aff_norm, const void *off_ins, void *pred_inter, void *pred,
+                               void *workspace, int B, int H, int W, int kh, int kw, int T, unsigned flags,
+                               void *stream) {
+    if (dtype != NLSPN_DTYPE_F32 && dtype != NLSPN_DTYPE_F16) return fail(NLSPN_EUNSUPPORTED, "dtype %d", dtype);
+    if (B < 1 || H < 1 || W < 1) return fail(NLSPN_EINVAL, "empty input: B=%d H=%d W=%d", B, H, W);
+    if (T < 1) return fail(NLSPN_EINVAL, "prop_time must be >= 1, got %d", T);
+    if (!p0 || !aff_norm || !off_ins || !pred_inter || !pred) return fail(NLSPN_EINVAL, "null required pointer");
+    const int K = kh * kw - 1;
+    const long long HW = (long long)H * W, N = (long long)B * HW;
+    const size_t es = esize(dtype);
+    hipStream_t s = as_stream(stream);
+    StepReq r{};
+    r.dtype = dtype;
+    r.kh = kh;
+    r.kw = kw;
+    r.a = StepArgs{p0, conf_eff, dep, aff_norm, off_ins, pred_inter, T == 1 ? pred : nullptr, (long long)(K + 1) * HW,
+                   2LL * (K + 1) * HW, B, H, W, 0, 0, NLSPN_OFF_INSERTED, flags, nullptr, nullptr, nullptr, nullptr, 0};
+    StepLaunch L;
+    if (int rc = prepare_step(r, L)) return rc;
+    ResPlan P;
+    const bool res = plan_resident(dtype, conf_eff, dep, aff_norm, off_ins, 2LL * (K + 1) * HW, pred_inter, pred,
+                                   workspace, B, H, W, kh, kw, T, flags | kResOffInserted, P);
+    StepArgs a1 = r.a;
+    if (res) {  // iteration 1 zeroes the resident kernel's progress words
+        a1.zero_words = P.a[0].sync;
+        a1.nzero = (int)(P.sync_bytes / 4);
+    }
+    if (int rc = launch(L, a1, s)) return rc;
+    if (res) return launch_resident(P, s);
+    for (int t = 1; t < T; ++t) {
+        StepArgs a = r.a;
+        a.p_in = static_cast<const char *>(pred_inter) + (size_t)(t - 1) * N * es;
+        a.p_out = static_cast<char *>(pred_inter) + (size_t)t * N * es;
+        a.pred_out = t == T - 1 ? pred : nullptr;
+        if (int rc = launch(L, a, s)) return rc;
+    }
+    return NLSPN_OK;
 }
 
 int nlspn_affinity_normalize(int dtype, const void *aff_raw, int64_t aff_bstride, const float *gamma,

@@ -46,6 +46,19 @@ struct HeadsArgs {
     float *pred_init;   // (B,1,H,W) or null
     float *conf;        // (B,1,H,W) or null
     int B, C, H, W, nout, tiles_x, tiles_y;
+    // The propagation prologue fused in (nlspnmodel.py:323-348; 3x3, K = 8 with offsets:
+    // nout = 24, one M-block), when aff_out is set: instead of the raw off_aff planes the
+    // epilogue writes the output-dict tensors — off_out = _off_insert(off) (:324),
+    // aff_out = _affinity_normalization + _aff_insert (:325), conf = the blended
+    // confidence (:328-334) — and p0, iteration 1's input (:341-348).  Same IEEE
+    // sequence as step 1 of nlspn_propagate (bit-identical given the same conv sums).
+    const float *dep;    // (B,1,H,W), or null (preserve_input off)
+    const float *gamma;  // device, 1 float (aff_scale_const)
+    float *aff_out;      // (B,K+1,H,W), or null: raw off_aff out
+    float *off_out;      // (B,2(K+1),H,W)
+    float *p0;           // (B,1,H,W)
+    int kind;
+    unsigned flags;      // NLSPN_PRESERVE_INPUT | NLSPN_ALWAYS_CLIP
     unsigned dbg;  // NLSPN_HEADS_DBG (ablation, timing only): 1 no VALU sums, 2 no MFMAs (both: the ABL
                    // kernels of MB=1), 4 no LDS staging
 };
@@ -59,6 +72,78 @@ template <int MB> struct HdCfg {
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// The fused-prologue epilogue of one MB = 1 workgroup (HeadsArgs::aff_out set; 3x3,
+// K = 8, nout = 24).  Lane (px, h) holds output channels co = (r&3) + 8(r>>2) + 4h of
+// pixel px: offsets co 0..15 in r 0..7, raw affinities 16..23 in r 8..11 (h = 0:
+// taps 0-3, h = 1: taps 4-7), the id conv in r 12 and the cf conv in r 13 (h = 0).
+// The two halves swap their four affinities (a 32-lane xor shuffle), so both hold the
+// pixel's eight in tap order and normalise them exactly as step 1 does (normalize_taps).
+__device__ __forceinline__ void heads_epilogue_prologue(const HeadsArgs &a, const f32x16 (&acc)[2],
+                                                        const float (&bv)[16], const float *SV, int b, int y0,
+                                                        int x, int wv, int h, int l32) {
+    constexpr int K = 8, REF = 4;
+    const int H = a.H, W = a.W;
+    const long long HW = (long long)H * W;
+    const bool preserve = (a.flags & 0x1u) != 0, clip = (a.flags & 0x2u) != 0;
+    const float gamma = *a.gamma;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const int yl = 2 * wv + n, y = y0 + yl;
+        if (y >= H || x >= W) continue;  // both halves of a pixel skip together
+        const long long pix = (long long)y * W + x;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[n][r] + bv[r];
+        // _off_insert (:252-259): raw channel c of tap c/2 -> inserted channel c + 2 past the reference tap
+        float *oo = a.off_out + (long long)b * 2 * (K + 1) * HW + pix;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+            oo[(long long)(co + (co >= 2 * REF ? 2 : 0)) * HW] = v[r];
+        }
+        if (h == 0) {
+            oo[(long long)(2 * REF) * HW] = 0.f;
+            oo[(long long)(2 * REF + 1) * HW] = 0.f;
+        }
+        // _affinity_normalization + _aff_insert (:179-201, :261-269)
+        float t[K][1], ref[1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float other = __shfl_xor(v[8 + i], 32);
+            t[i][0] = h == 0 ? v[8 + i] : other;
+            t[4 + i][0] = h == 0 ? other : v[8 + i];
+        }
+        normalize_taps<K, 1>(t, ref, a.kind, gamma);
+        float *ao = a.aff_out + (long long)b * (K + 1) * HW + pix;
+        if (h == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ao[(long long)k * HW] = t[k][0];
+            ao[(long long)REF * HW] = ref[0];
+        } else {
+#pragma unroll
+            for (int k = 4; k < K; ++k) ao[(long long)(k + 1) * HW] = t[k][0];
+        }
+        // pred_init, p0 and the blended confidence (:297, :313, :328-348)
+        if (h == 0) {
+            const float d = preserve ? a.dep[(long long)b * HW + pix] : 0.f;
+            const float m = d > 0.f ? 1.f : 0.f;
+            const float u = v[12] + SV[yl * kHdTW + l32];
+            const float pi = u < 0.f ? 0.f : u;  // ReLU (NaN kept)
+            a.pred_init[(long long)b * HW + pix] = pi;
+            float p = pi;
+            if (preserve) p = __fadd_rn(__fmul_rn(1.0f - m, p), __fmul_rn(m, d));
+            if (clip) p = clamp0(p);
+            a.p0[(long long)b * HW + pix] = p;
+            if (a.conf) {
+                const float uc = v[13] + SV[kHdNT + yl * kHdTW + l32];
+                float c = 1.f / (1.f + expf(-uc));  // Sigmoid
+                if (preserve) c = __fadd_rn(__fmul_rn(1.0f - m, c), m);
+                a.conf[(long long)b * HW + pix] = c;
+            }
+        }
+    }
+}
 
 // One input window of a chunk (16 channels x 10 rows x 40 columns) in flight in
 // registers: raw bits + a per-float4 in-image mask.  Every lane loads a clamped,
@@ -225,7 +310,7 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
                 }
                 if constexpr (decltype(do_valu)::value) {
 #pragma unroll
-                    for (int e = 0; e < 2; ++e) sacc[e] += xv[cur][e] * wv2[cur][e];
+                    for (int e = 0; e < 2; ++e) sacc[e] = fmaf(xv[cur][e], wv2[cur][e], sacc[e]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -247,6 +332,12 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
     for (int m = 0; m < MB; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) bv[m][r] = a.bias[32 * m + (r & 3) + 8 * (r >> 2) + 4 * h];
+    if constexpr (MB == 1) {
+        if (a.aff_out) {
+            heads_epilogue_prologue(a, acc[0], bv[0], SV, b, y0, x, wv, h, l32);
+            return;
+        }
+    }
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         const int yl = 2 * wv + n, y = y0 + yl;

@@ -1,7 +1,6 @@
 // Device code of the head-epilogue convolution kernel (nlspn_heads.h), its own
-// translation unit: built with contraction on (the VALU part's multiply-adds are
-// plain f32 FMAs; the propagation kernels keep -ffp-contract=off for bit parity
-// with the oracle, which this kernel does not claim).  Launched from nlspn_capi.hip.
+// translation unit (it rebuilds in parallel with nlspn_capi.hip).  Launched from
+// nlspn_capi.hip.
 #include "nlspn_heads.h"
 
 namespace nlspn {

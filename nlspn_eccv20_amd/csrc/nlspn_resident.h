@@ -62,7 +62,7 @@ struct ResArgs {
     const void *conf;   // conf' of this launch's images (planes H*W apart), or null (conf_prop off)
     const void *dep;    // planes H*W apart, or null (preserve off)
     const void *aff;    // normalised affinity, (K+1) planes per item, contiguous (aff_out)
-    const void *off;    // raw offsets, 2K planes per item, batch stride off_bs
+    const void *off;    // offsets, batch stride off_bs: raw 2K planes, or inserted 2(K+1) (flags kResOffInserted)
     void *pred_inter;   // plane (t, b) at t * tstride + b * H * W: iteration t reads t-1, writes t
     void *pred;         // planes H*W apart: max(p_T, 0) (nlspnmodel.py:375-377)
     unsigned *sync;     // [0] abort word, [1 + blockIdx] progress words; zeroed by step 1
@@ -104,6 +104,7 @@ constexpr bool kResGeneralPath = true;
 constexpr bool kResGeneralPath = false;  // experiment only: wrong results for taps outside the window
 #endif
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
+constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 
 // Band i of n over a length L owns [i*L/n, (i+1)*L/n); owner(v) is the largest i
 // with floor(i*L/n) <= v.
@@ -220,6 +221,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
+    const bool off_ins = (a.flags & kResOffInserted) != 0;
     const long long HW = (long long)H * W;
     const unsigned plane_bytes = (unsigned)HW * ES;
     gu32 *sync = (gu32 *)(a.sync);
@@ -248,8 +250,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             ResVec<T>::template load<0>(ra_, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, ak[k]);
-            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * k) * plane_bytes, hy[k]);
-            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * k + 1) * plane_bytes, hx[k]);
+            const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
+            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
+            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) dv[e] = 0.f;
@@ -561,10 +564,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                         const float4 a4 = akl[k];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
                         const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
+                        const int ok = (off_ins && k >= REF) ? k + 1 : k;
                         const float h_im = (float)(y - PH + i) +
-                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * k) * plane_bytes);
+                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok) * plane_bytes);
                         const float w_im = (float)(x0 + e - PW + jj) +
-                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * k + 1) * plane_bytes);
+                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok + 1) * plane_bytes);
                         float v = 0.f;
                         if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                             const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);

@@ -59,7 +59,7 @@ struct StepArgs {
     void *off_out;       // 2(K+1) planes per item, contiguous, or null
     void *conf_out;      // B planes, or null iff conf null
     int kind;            // affinity kind
-    unsigned *zero_words;  // FIRST: progress words of the resident kernel that follows, zeroed here
+    unsigned *zero_words;  // step 1: progress words of the resident kernel that follows, zeroed here
     int nzero;             //   (replaces a memset node; the kernel boundary orders it)
 };
 
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     const int x0 = tx * TW, y0 = ty * TH;
     const int wy0 = y0 - RY, wx0 = x0 - RX;
 
-    if (FIRST && a.zero_words && blockIdx.x == 0)
+    if (a.zero_words && blockIdx.x == 0)  // step 1 (either form) zeroes the resident kernel's words
         for (int i = threadIdx.x; i < a.nzero; i += NT)
             __hip_atomic_store(a.zero_words + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool has_conf = a.conf != nullptr;

@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from . import _lib
 
-__all__ = ["head_epilogue", "HeadWeights"]
+__all__ = ["head_epilogue", "head_epilogue_prologue", "HeadWeights"]
 
 
 def _stream(device):
@@ -132,3 +132,47 @@ def head_epilogue(fe1, off_aff_fd1, off_aff_dec0, id_fd1=None, id_dec0=None, cf_
             _lib.DTYPE_F32, *[_p(t) for t in srcs], _p(weights.wm), _p(weights.wv), _p(weights.bias), _p(off_aff),
             _p(pred_init), _p(conf), B, C, H, W, weights.nout, _stream(dev)))
     return pred_init, off_aff, conf
+
+
+def head_epilogue_prologue(fe1, off_aff_fd1, off_aff_dec0, id_fd1, id_dec0, dep, gamma, affinity="TGASS",
+                           cf_fd1=None, cf_dec0=None, preserve_input=True, always_clip=False,
+                           weights: HeadWeights | None = None) -> dict:
+    """The three head convolutions with the propagation prologue fused into their
+    epilogue (3x3, K = 8, offsets on; nlspnmodel.py:297-348): returns {'pred_init',
+    'offset' (_off_insert, :324), 'aff' (normalised + reference tap, :325),
+    'confidence' (blended, :328-334, or None), 'p0' (iteration 1's input, :341-348)} —
+    what nlspn_propagate's step 1 would produce from the raw head outputs, bit for bit.
+    Feed them to propagation.propagate_normalized."""
+    from .propagation import _gamma_f32
+    oa, idc, cfc = _conv_of(off_aff_dec0), _conv_of(id_dec0), _conv_of(cf_dec0)
+    if (cf_fd1 is None) != (cfc is None) or id_fd1 is None or idc is None:
+        raise RuntimeError("the fused prologue needs id_fd1/id_dec0, and cf_fd1 with cf_dec0")
+    if oa.out_channels != 24:
+        raise RuntimeError("the fused prologue is the 3x3 / K=8 / offset geometry (off_aff_dec0 -> 24 channels)")
+    from . import _lib as L
+    if affinity not in L.AFF_KINDS:
+        raise NotImplementedError(affinity)
+    weights = (weights or HeadWeights()).get(oa, idc, cfc)
+    B, C, H, W = fe1.shape
+    srcs = [fe1, off_aff_fd1, id_fd1, cf_fd1]
+    for n, t in zip(("fe1", "off_aff_fd1", "id_fd1", "cf_fd1"), srcs):
+        if t is None:
+            continue
+        if not t.is_cuda or t.dtype != torch.float32 or tuple(t.shape) != (B, C, H, W):
+            raise RuntimeError(f"{n} must be a float32 CUDA tensor of shape {(B, C, H, W)}")
+    if preserve_input and (dep is None or tuple(dep.shape) != (B, 1, H, W)):
+        raise RuntimeError("preserve_input requires dep of shape (B, 1, H, W)")
+    srcs = [None if t is None else t.contiguous() for t in srcs]
+    dep = None if dep is None else dep.contiguous().float()
+    g = _gamma_f32(gamma)
+    dev = fe1.device
+    e = lambda c: torch.empty((B, c, H, W), dtype=torch.float32, device=dev)  # noqa: E731
+    out = {"pred_init": e(1), "offset": e(18), "aff": e(9), "confidence": e(1) if cf_fd1 is not None else None,
+           "p0": e(1)}
+    flags = (L.PRESERVE_INPUT if preserve_input else 0) | (L.ALWAYS_CLIP if always_clip else 0)
+    with torch.cuda.device(dev):
+        L.check(L.get().nlspn_head_epilogue_prologue(
+            L.DTYPE_F32, *[_p(t) for t in srcs], _p(weights.wm), _p(weights.wv), _p(weights.bias), _p(dep), _p(g),
+            _p(out["pred_init"]), _p(out["confidence"]), _p(out["aff"]), _p(out["offset"]), _p(out["p0"]),
+            B, C, H, W, 3, 3, L.AFF_KINDS[affinity], flags, _stream(dev)))
+    return out

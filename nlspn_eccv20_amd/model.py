@@ -23,8 +23,9 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .propagation import affinity_normalization, kernel_geometry, off_insert, prop_step, propagate
-from .heads import HeadWeights, head_epilogue
+from .propagation import (affinity_normalization, kernel_geometry, off_insert, prop_step, propagate,
+                          propagate_normalized)
+from .heads import HeadWeights, head_epilogue, head_epilogue_prologue
 from .s2d import s2d_front
 
 __all__ = ["NLSPNModel", "ConvGRU", "S2D", "conv_bn_relu", "convt_bn_relu", "get_resnet18", "get_resnet34", "get",
@@ -276,8 +277,9 @@ class NLSPNModel(nn.Module):
         """nlspnmodel.py:161-177: crop decoder padding, then concatenate."""
         return torch.cat((cls._crop(fd, fe), fe), dim=dim)
 
-    def heads(self, sample):
-        """Encoder + decoder heads, nlspnmodel.py:272-315: (pred_init, off_aff, confidence)."""
+    def _decoder(self, sample):
+        """Encoder + shared decoder + the heads' first layers, nlspnmodel.py:272-312:
+        (fe1, id_fd1, off_aff_fd1, cf_fd1 or None), the decoder outputs cropped to fe1."""
         rgb, dep = sample["rgb"], sample["dep"]
         fe1_rgb = self.conv1_rgb(rgb)
         fe1_dep = self.S2D(dep) if self.args.use_S2D else self.conv1_dep(dep)
@@ -292,18 +294,25 @@ class NLSPNModel(nn.Module):
         id_fd1 = self.id_dec1(self._concat(fd2, fe2))
         off_aff_fd1 = self.off_aff_dec1(self._concat(fd2, fe2))
         cf_fd1 = self.cf_dec1(self._concat(fd2, fe2)) if self.args.conf_prop else None
-        if fe1.is_cuda and not torch.is_grad_enabled() and fe1.dtype == torch.float32:
+        crop = lambda fd: None if fd is None else self._crop(fd, fe1)  # noqa: E731
+        return fe1, crop(id_fd1), crop(off_aff_fd1), crop(cf_fd1)
+
+    def _fused_inference(self, fe1) -> bool:
+        return fe1.is_cuda and not torch.is_grad_enabled() and fe1.dtype == torch.float32
+
+    def heads(self, sample):
+        """Encoder + decoder heads, nlspnmodel.py:272-315: (pred_init, off_aff, confidence)."""
+        fe1, id_fd1, off_aff_fd1, cf_fd1 = self._decoder(sample)
+        if self._fused_inference(fe1):
             # inference: the three last convolutions + bias/activation as one HIP kernel
             # reading fe1 and the decoder outputs in place (heads.py, nlspn_heads.h)
-            crop = lambda fd: None if fd is None else self._crop(fd, fe1)  # noqa: E731
-            return head_epilogue(fe1, crop(off_aff_fd1), self.off_aff_dec0, crop(id_fd1), self.id_dec0,
-                                 crop(cf_fd1), self.cf_dec0 if self.args.conf_prop else None,
-                                 weights=self._head_weights)
-        pred_init = self.id_dec0(self._concat(id_fd1, fe1))
-        off_aff = self.off_aff_dec0(self._concat(off_aff_fd1, fe1))
+            return head_epilogue(fe1, off_aff_fd1, self.off_aff_dec0, id_fd1, self.id_dec0, cf_fd1,
+                                 self.cf_dec0 if self.args.conf_prop else None, weights=self._head_weights)
+        pred_init = self.id_dec0(torch.cat((id_fd1, fe1), 1))
+        off_aff = self.off_aff_dec0(torch.cat((off_aff_fd1, fe1), 1))
         confidence = None
         if self.args.conf_prop:
-            confidence = self.cf_dec0(self._concat(cf_fd1, fe1))
+            confidence = self.cf_dec0(torch.cat((cf_fd1, fe1), 1))
         return pred_init, off_aff, confidence
 
     def _aff_head(self, aff_feat):
@@ -313,8 +322,39 @@ class NLSPNModel(nn.Module):
         return affinity_normalization(aff, self.aff_scale_const, self.args.affinity)
 
     def forward(self, sample):
+        a = self.args
+        if (not a.use_GRU and a.offset and (self.kh, self.kw) == (3, 3) and a.affinity in ("AS", "ASS", "TC", "TGASS")
+                and torch.cuda.is_available() and sample["dep"].is_cuda and not torch.is_grad_enabled()):
+            fe1, id_fd1, off_aff_fd1, cf_fd1 = self._decoder(sample)
+            if self._fused_inference(fe1):
+                return self._forward_fused(fe1, id_fd1, off_aff_fd1, cf_fd1, sample["dep"])
+            return self.propagate_heads(*self._heads_from(fe1, id_fd1, off_aff_fd1, cf_fd1), sample["dep"])
         pred_init, off_aff, confidence = self.heads(sample)
         return self.propagate_heads(pred_init, off_aff, confidence, sample["dep"])
+
+    def _heads_from(self, fe1, id_fd1, off_aff_fd1, cf_fd1):
+        pred_init = self.id_dec0(torch.cat((id_fd1, fe1), 1))
+        off_aff = self.off_aff_dec0(torch.cat((off_aff_fd1, fe1), 1))
+        confidence = self.cf_dec0(torch.cat((cf_fd1, fe1), 1)) if self.args.conf_prop else None
+        return pred_init, off_aff, confidence
+
+    def _forward_fused(self, fe1, id_fd1, off_aff_fd1, cf_fd1, dep):
+        """Inference, 3x3 / K=8 / offsets (the reference's NYU and KITTI models): the head
+        convolutions with the propagation prologue fused into their epilogue
+        (heads.head_epilogue_prologue: _off_insert, the affinity normalisation, the
+        confidence / input blend, :296-348), then the loop from the prologued planes
+        (propagation.propagate_normalized, :340-381).  The same output dict as
+        propagate_heads, bit for bit given the same convolution sums."""
+        a = self.args
+        h = head_epilogue_prologue(fe1, off_aff_fd1, self.off_aff_dec0, id_fd1, self.id_dec0, dep,
+                                   self.aff_scale_const, a.affinity, cf_fd1,
+                                   self.cf_dec0 if a.conf_prop else None, a.preserve_input, a.always_clip,
+                                   weights=self._head_weights)
+        o = propagate_normalized(h["p0"], dep if a.preserve_input else None, h["confidence"], h["aff"],
+                                 h["offset"], a.prop_time, (3, 3), a.preserve_input, a.always_clip)
+        return {"pred": o["pred"], "pred_init": h["pred_init"], "pred_inter": o["pred_inter"],
+                "offset": h["offset"], "aff": h["aff"], "gamma": self.aff_scale_const.data,
+                "confidence": h["confidence"]}
 
     def propagate_heads(self, pred_init, off_aff, confidence, dep):
         """The propagation section, nlspnmodel.py:303-383, on the heads' outputs."""

@@ -431,6 +431,41 @@ def propagate(pred_init: torch.Tensor, dep: Optional[torch.Tensor], confidence: 
             "confidence": conf_o, "pred_inter_tensor": pred_inter}
 
 
+def propagate_normalized(p0: torch.Tensor, dep: Optional[torch.Tensor], confidence: Optional[torch.Tensor],
+                         aff: torch.Tensor, offset: torch.Tensor, prop_time: int = 18, kernel=3,
+                         preserve_input: bool = True, always_clip: bool = False) -> dict:
+    """The propagation loop (nlspnmodel.py:340-381) from prologued inputs: p0 (the
+    blended [clamped] pred_init iteration 1 propagates), the blended confidence, the
+    normalised (K+1)-tap affinity and the inserted 2(K+1)-plane offsets — what
+    heads.head_epilogue_prologue writes (or propagate's own step 1).  Inference only.
+    Returns {'pred', 'pred_inter' (T views), 'pred_inter_tensor'}."""
+    kh, kw = kernel_geometry(kernel)
+    K = kh * kw - 1
+    for n, t in (("p0", p0), ("dep", dep), ("confidence", confidence), ("aff", aff), ("offset", offset)):
+        _cuda(n, t)
+    B, _, H, W = p0.shape
+    dt = p0.dtype
+    for n, t, c in (("p0", p0, 1), ("dep", dep, 1), ("confidence", confidence, 1), ("aff", aff, K + 1),
+                    ("offset", offset, 2 * (K + 1))):
+        if t is not None and (tuple(t.shape) != (B, c, H, W) or not t.is_contiguous() or t.dtype != dt):
+            raise RuntimeError(f"{n} must be a contiguous {(B, c, H, W)} tensor of p0's dtype")
+    if preserve_input and dep is None:
+        raise RuntimeError("preserve_input requires dep")
+    T = int(prop_time)
+    kw_ = dict(dtype=dt, device=p0.device)
+    pred_inter = torch.empty((T, B, 1, H, W), **kw_)
+    pred = torch.empty((B, 1, H, W), **kw_)
+    ws = torch.empty(_lib.get().nlspn_workspace_bytes(_dtype_code(p0), B, H, W) // 4, dtype=torch.int32,
+                     device=p0.device)
+    flags = (_lib.PRESERVE_INPUT if preserve_input else 0) | (_lib.ALWAYS_CLIP if always_clip else 0)
+    with torch.cuda.device(p0.device):
+        _lib.check_resident()
+        _lib.check(_lib.get().nlspn_propagate_normalized(
+            _dtype_code(p0), _ptr(p0), _ptr(dep), _ptr(confidence), _ptr(aff), _ptr(offset), _ptr(pred_inter),
+            _ptr(pred), _ptr(ws), B, H, W, kh, kw, T, flags, _stream(p0.device)))
+    return {"pred": pred, "pred_inter": list(pred_inter.unbind(0)), "pred_inter_tensor": pred_inter}
+
+
 class PropagationPlan:
     """propagate() captured once (nlspn_plan_create) over fixed input/output buffers;
     replay() re-runs the whole section (the recorded launches re-issued directly, or
