@@ -55,3 +55,24 @@ def test_head_epilogue_rejects_cpu_tensors():
         head_epilogue(x, x, oa)
     with pytest.raises(RuntimeError, match="both its decoder output"):
         head_epilogue(x, x, oa, id_fd1=x)
+
+
+def test_fused_prologue_host_checks():
+    """The fused-prologue entry points refuse what their kernels do not take (CPU
+    tensors, a missing id head, a non-K=8 head) before any launch."""
+    from nlspn_eccv20_amd import _lib, propagate_normalized
+    from nlspn_eccv20_amd.heads import head_epilogue_prologue
+    try:
+        _lib.get()
+    except (ImportError, OSError):
+        pytest.skip("HIP library not built")
+    x = torch.zeros((1, 1, 8, 8))
+    with pytest.raises(RuntimeError, match="CUDA"):
+        propagate_normalized(x, x, x, torch.zeros((1, 9, 8, 8)), torch.zeros((1, 18, 8, 8)), 3)
+    oa = nn.Conv2d(32, 24, 3, padding=1)
+    f = torch.zeros((1, 16, 8, 8))
+    with pytest.raises(RuntimeError, match="id_fd1"):
+        head_epilogue_prologue(f, f, oa, None, None, x, torch.ones(1))
+    with pytest.raises(RuntimeError, match="K=8"):
+        head_epilogue_prologue(f, f, nn.Conv2d(32, 48, 3, padding=1), f, nn.Conv2d(32, 1, 3, padding=1), x,
+                               torch.ones(1))
