@@ -391,10 +391,33 @@ def head_epilogue_timing(cfg, dev, reps=20):
             ts.append(e0.elapsed_time(e1))
         return statistics.median(ts)
 
+    # heads + propagation section: raw epilogue then nlspn_propagate (step 1 normalises)
+    # vs the epilogue with the prologue fused in then nlspn_propagate_normalized
+    from nlspn_eccv20_amd import propagate, propagate_normalized
+    from nlspn_eccv20_amd.heads import head_epilogue_prologue
+    dep = torch.rand((B, 1, H, W), device=dev, generator=g) * cfg["max_depth"]
+    dep = dep * (torch.rand((B, 1, H, W), device=dev, generator=g) < cfg["density"])
+    gamma = torch.tensor([0.5 * K], device=dev)
+    kern = cfg["kernel"]
+
+    def unfused_section():
+        pi, oa_out, co = fused()
+        return propagate(pi, dep, co, oa_out[:, 2 * K:], oa_out[:, :2 * K], gamma, prop_time=cfg["T"],
+                         kernel=kern)["pred"]
+
+    def fused_section():
+        h = head_epilogue_prologue(fe1, oa_fd1, oa, id_fd1, idc, dep, gamma, "TGASS", cf_fd1, cfc, weights=hw)
+        return propagate_normalized(h["p0"], dep, h["confidence"], h["aff"], h["offset"], cfg["T"], kern)["pred"]
+
     with torch.no_grad():
         t_fused, t_ref = med(fused), med(ref)
         f, r = fused(), ref()
         diff = max((a - b).abs().max().item() for a, b in zip(f, r))
+        sec = {}
+        if kern == (3, 3):
+            sec = {"ms_heads_then_propagate": round(med(unfused_section), 4),
+                   "ms_heads_prologue_then_loop": round(med(fused_section), 4),
+                   "bit_identical_pred": bool(torch.equal(unfused_section(), fused_section()))}
     del fe1, id_fd1, oa_fd1, cf_fd1
     flops = 2.0 * B * H * W * 128 * 9 * (3 * K + 2)
     ach = flops / (t_fused * 1e-3) / 1e12
@@ -404,8 +427,11 @@ def head_epilogue_timing(cfg, dev, reps=20):
                          "frac": round(ach / 157.3, 3),
                          "basis": "useful FLOPs 2*B*H*W*128*9*(3K+2) / fused-call time; peak = f32-input MFMA "
                                   "(v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md)"},
+            "with_section": sec,
             "note": "fused: one HIP kernel (nlspn_heads.h, f32 operands on the matrix cores), reads fe1 + decoder "
-                    "outputs in place; torch: 3 x (torch.cat + MIOpen conv) + ReLU/Sigmoid"}
+                    "outputs in place; torch: 3 x (torch.cat + MIOpen conv) + ReLU/Sigmoid; with_section: the heads "
+                    "then the T-iteration section, eager, raw epilogue + nlspn_propagate vs the epilogue with the "
+                    "prologue fused in + nlspn_propagate_normalized"}
 
 
 def cpu_model():
