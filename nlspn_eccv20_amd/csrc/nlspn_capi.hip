@@ -41,6 +41,8 @@ NLSPN_HD_EXTERN(5)
 extern template __global__ void heads_kernel<1, true, 1>(HeadsArgs);
 extern template __global__ void heads_kernel<1, true, 2>(HeadsArgs);
 extern template __global__ void heads_kernel<1, true, 3>(HeadsArgs);
+extern template __global__ void heads_kernel<1, true, 0, true>(HeadsArgs);
+extern template __global__ void heads_kernel<1, false, 0, true>(HeadsArgs);
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -668,7 +670,10 @@ static int launch_heads(HeadsArgs &a, void *stream) {
 #undef NLSPN_HD_CASE
         default: return fail(NLSPN_EUNSUPPORTED, "head epilogue: nout=%d", nout);
     }
-    if (vec && head_mb(nout) == 1 && (a.dbg & 3u)) {  // ablation kernels (timing only)
+    if (a.aff_out)  // the fused propagation prologue (nout = 24: MB = 1)
+        fn = vec ? reinterpret_cast<const void *>(&heads_kernel<1, true, 0, true>)
+                 : reinterpret_cast<const void *>(&heads_kernel<1, false, 0, true>);
+    else if (vec && head_mb(nout) == 1 && (a.dbg & 3u)) {  // ablation kernels (timing only)
         const void *abl[3] = {reinterpret_cast<const void *>(&heads_kernel<1, true, 1>),
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 2>),
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 3>)};

@@ -197,7 +197,7 @@ template <bool VEC> struct HdWin {
 // body as the channel pair's 18 MFMAs, so they issue in the matrix cores' shadow.  An
 // absent id / cf source is replaced by fe1 (valid memory) and its sum discarded: every
 // round runs the same straight-line code.
-template <int MB, bool VEC, int ABL = 0>
+template <int MB, bool VEC, int ABL = 0, bool PRO = false>
 __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2))) heads_kernel(HeadsArgs a) {
     using Cfg = HdCfg<MB>;
     constexpr int NCO = Cfg::NCO, WCS = Cfg::WCS;
@@ -332,11 +332,10 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
     for (int m = 0; m < MB; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) bv[m][r] = a.bias[32 * m + (r & 3) + 8 * (r >> 2) + 4 * h];
-    if constexpr (MB == 1) {
-        if (a.aff_out) {
-            heads_epilogue_prologue(a, acc[0], bv[0], SV, b, y0, x, wv, h, l32);
-            return;
-        }
+    if constexpr (PRO) {  // the fused propagation prologue (its own instantiation: no registers for the other)
+        static_assert(MB == 1, "3x3 / K = 8 only");
+        heads_epilogue_prologue(a, acc[0], bv[0], SV, b, y0, x, wv, h, l32);
+        return;
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n) {

@@ -15,4 +15,7 @@ NLSPN_HD_INST(5)
 template __global__ void heads_kernel<1, true, 1>(HeadsArgs);
 template __global__ void heads_kernel<1, true, 2>(HeadsArgs);
 template __global__ void heads_kernel<1, true, 3>(HeadsArgs);
+// the fused propagation prologue (nlspn_head_epilogue_prologue)
+template __global__ void heads_kernel<1, true, 0, true>(HeadsArgs);
+template __global__ void heads_kernel<1, false, 0, true>(HeadsArgs);
 }  // namespace nlspn
