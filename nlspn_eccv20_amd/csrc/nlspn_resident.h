@@ -433,15 +433,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const int d = base + lane;
                 const int dy = d / ndx;
                 const int jj = (dy0 + dy) * a.gx + dx0 + (d - dy * ndx);
+                // lanes without a dependency watch the abort word in the same wave load,
+                // so a spin is ONE memory round trip (a separate abort load per spin, issued
+                // after the ballot, doubled the poll period)
+                const bool spare = base + 64 > ndep;
+                gu32 *wp = d < ndep ? &sync[1 + xcd_unmap(b * nparts + jj, G)] : &sync[0];
                 for (;;) {
-                    bool ok = true;
-                    if (d < ndep)
-                        ok = __hip_atomic_load(&sync[1 + xcd_unmap(b * nparts + jj, G)], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) >=
-                             need;
-                    if (__all(ok)) break;
-                    if (++spins > kResSpinLimit ||
-                        __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                    const unsigned v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(d >= ndep || v >= need)) break;
+                    if (__any(d >= ndep && v != 0u) || ++spins > kResSpinLimit ||
+                        (!spare && (spins & 15u) == 0u &&
+                         __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
                         fail = true;
                         break;
                     }
