@@ -50,14 +50,16 @@ def test_s2d_weight_gradients_vs_torch():
     dep, w1, b1, w2, b2 = (a.to(DEV) for a in _case(2, 64, 96, 0.05, seed=9))
     params = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
     out = s2d_front(dep, *params)
-    g = torch.randn_like(out)
+    g = torch.randn(out.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
     grads = torch.autograd.grad(out, params, g)
     _, pyr = O.s2d_front(*(a.cpu().numpy() for a in (dep, w1, b1, w2, b2)))
     rp = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
     h = F.relu(F.conv2d(F.relu(F.conv2d(torch.from_numpy(pyr).to(DEV), rp[0], rp[1])), rp[2], rp[3]))
     ref = torch.autograd.grad(h, rp, g[:, :16])
+    # both sides are MIOpen weight-gradient reductions over 12,288 pixels (its
+    # algorithms may accumulate in different orders run to run): f32 reduction bar
     for a, r in zip(grads, ref):
-        torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(a, r, rtol=1e-3, atol=1e-3)
 
 
 def test_model_s2d_uses_kernel_and_matches_cpu_module():
