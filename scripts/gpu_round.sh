@@ -19,6 +19,13 @@ NLSPN_RESIDENT=0 timeout -k 10 300 python bench.py --no-backward --no-gru --no-e
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o bench --output-format csv -- \
     python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru > $O/stats.log 2>&1 || exit 1
+# kernel stats per config (kernels are shared between configs, so the default run's
+# averages mix them): each bench config alone, for the roofline cross-check
+for CFG in nyu kitti nyu_k16; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_$CFG -o bench --output-format csv -- \
+      python3 $R/bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru --no-heads \
+      --no-extra-configs > $O/stats_$CFG.log 2>&1 || exit 1
+done
 # PMC HBM traffic, one config per pass pair (kernels are shared between configs)
 for CFG in nyu kitti nyu_k16; do
   for C in FETCH_SIZE WRITE_SIZE; do
