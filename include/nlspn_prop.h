@@ -57,6 +57,9 @@ extern "C" {
 #define NLSPN_EUNSUPPORTED 2 /* geometry or dtype without a kernel instantiation */
 #define NLSPN_EHIP 3         /* HIP runtime / launch error */
 #define NLSPN_EABORTED 4     /* a resident launch aborted (nlspn_resident_status) */
+/* nlspn_time_propagate *resident: bit set when iteration 1 ran inside the resident
+ * launches (no step-1 kernel; *first_ms is then ~0) */
+#define NLSPN_RESIDENT_FIRST 0x100
 
 /* Version of this ABI (NLSPN_ABI_VERSION). */
 int nlspn_abi_version(void);
@@ -174,8 +177,10 @@ size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
  *              words in `workspace` — when the geometry allows it (3x3 learned
  *              offsets, W % 4 == 0, 16-B aligned planes, every rectangular part fits
  *              a workgroup: nlspn_resident_config), else T-1 nlspn_prop_step
- *              launches; pred_inter[t] each, the last also pred.  Both forms are
- *              bit-identical.
+ *              launches; pred_inter[t] each, the last also pred.
+ *   NLSPN_RES_FIRST=1: step 1 moves into the resident launches too (their setup runs
+ *   the prologue, a memset node zeroes the progress words; measured slower, kept as
+ *   an A/B).  Every form is bit-identical.
  * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
  *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
  *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
@@ -327,7 +332,9 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
  * around every launch, synchronise, and return the mean duration of step 1
  * (first_ms) and of iterations 2..T (rest_ms: from the start of the first
  * resident launch to the end of the last, or the sum of the T-1 step kernels);
- * *resident = the number of resident launches (image groups), 0 for step launches.
+ * *resident = the number of resident launches (image groups), 0 for step launches,
+ * | NLSPN_RESIDENT_FIRST when those launches also ran iteration 1 (rest_ms then spans
+ * iterations 1..T).
  */
 int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
                          const void *aff_raw, int64_t aff_bstride, const void *off_raw,

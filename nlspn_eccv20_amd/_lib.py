@@ -21,6 +21,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nlspn_prop.h")
 DTYPE_F32, DTYPE_F16, DTYPE_F64 = 0, 1, 2  # F64: the seam-2 DCN entry points only
 AFF_KINDS = {"AS": 0, "ASS": 1, "TC": 2, "TGASS": 3}
 PRESERVE_INPUT, ALWAYS_CLIP = 0x1, 0x2
+RESIDENT_FIRST = 0x100  # nlspn_time_propagate *resident: iteration 1 ran inside the resident launches
 OFF_INSERTED, OFF_RAW = 0, 1
 EINVAL, EUNSUPPORTED, EHIP, EABORTED = 1, 2, 3, 4
 

@@ -167,12 +167,14 @@ int prepare_step(StepReq &r, StepLaunch &L) {
 
 // A plan's launch record: enough to re-issue one kernel launch without a graph.
 struct LaunchRec {
-    const void *fn;
+    const void *fn;  // null: a memset of zbytes at zptr (the resident kernel's progress words)
     dim3 grid, block;
     size_t lds;
     bool resident;
     StepArgs sa;
     ResArgs ra;
+    void *zptr = nullptr;
+    size_t zbytes = 0;
 };
 thread_local std::vector<LaunchRec> *g_rec = nullptr;  // set while nlspn_plan_create records
 
@@ -298,6 +300,7 @@ struct ResPlan {
     unsigned block = 0;
     size_t lds = 0, sync_bytes = 0;
     int ngroups = 0;
+    bool first = false;  // iteration 1 runs in the launches (ResFirstIn)
     unsigned grid[kResMaxGroups] = {};
     ResArgs a[kResMaxGroups];
 };
@@ -353,16 +356,30 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
     return false;
 }
 
-// Fills P and returns true when the resident kernel applies.
+// Iteration 1 and the forward prologue inside the resident launches (ResArgs kResFirst):
+// the raw inputs step 1 would read; conf_eff / aff_norm of plan_resident are then the
+// conf_out / aff_out the launches write.
+struct ResFirstIn {
+    const void *pinit, *conf_raw, *aff_raw;
+    long long aff_bs;
+    void *off_out;
+    const float *gamma;
+    int kind;
+};
+
+// Fills P and returns true when the resident kernel applies (with F: iterations 1..T).
 bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
-                   int kw, int T, unsigned flags, ResPlan &P) {
+                   int kw, int T, unsigned flags, ResPlan &P, const ResFirstIn *F = nullptr) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
     const size_t es = esize(dtype), vb = 4 * es;
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
+        return false;
+    if (F && (!aligned(F->pinit, vb) || !aligned(F->conf_raw, vb) || !aligned(F->aff_raw, vb) || F->aff_bs % 4 != 0 ||
+              !aligned(F->off_out, vb) || !F->gamma || ((flags & kPreserve) && !dep)))
         return false;
     const int cus = device_cus();
     if (cus < 1) return false;
@@ -403,19 +420,42 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
             return p ? static_cast<const char *>(p) + (size_t)(elems * (long long)es) : nullptr;
         };
         P.grid[k] = (unsigned)(Bk * S.gy * S.gx);
+        // progress values of group k: epoch + 1 .. epoch + T, epoch = k (T + 1)
         P.a[k] = ResArgs{at(conf_eff, b0 * HW), (flags & kPreserve) ? at(dep, b0 * HW) : nullptr,
                          at(aff_norm, b0 * (K + 1) * HW), at(off_raw, b0 * off_bs),
                          const_cast<void *>(at(pred_inter, b0 * HW)), const_cast<void *>(at(pred, b0 * HW)),
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
-                         Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * T), flags, dbg};
+                         Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)), flags, dbg};
+        if (F) {
+            ResArgs &r = P.a[k];
+            r.flags |= kResFirst;
+            r.pinit = at(F->pinit, b0 * HW);
+            r.conf_raw = at(F->conf_raw, b0 * HW);
+            r.aff_raw = at(F->aff_raw, b0 * F->aff_bs);
+            r.aff_bs = F->aff_bs;
+            r.off_out = const_cast<void *>(at(F->off_out, b0 * 2 * (K + 1) * HW));
+            r.gamma = F->gamma;
+            r.kind = F->kind;
+        }
     }
+    P.first = F != nullptr;
     return true;
 }
 
-// The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words).
+// The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words),
+// or (P.first: no step 1) a memset node here.
 // e0 is recorded at the start of the first group's launch, e1 at the end of the last.
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
+    if (P.first) {
+        if (g_rec) {
+            LaunchRec z{};
+            z.zptr = P.a[0].sync;
+            z.zbytes = P.sync_bytes;
+            g_rec->push_back(z);
+        }
+        NLSPN_HIP_TRY(hipMemsetAsync(P.a[0].sync, 0, P.sync_bytes, s));
+    }
     for (int k = 0; k < P.ngroups; ++k) {
         if (g_rec)
             g_rec->push_back(LaunchRec{P.fn, dim3(P.grid[k]), dim3(P.block), P.lds, true, StepArgs{}, P.a[k]});
@@ -550,6 +590,23 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
 
     if (resident) *resident = 0;
     ResPlan P;
+    // NLSPN_RES_FIRST=1: iterations 1..T resident, the prologue in the launches' setup
+    // (no step-1 launch).  Bit-identical, but not the default: measured slower (C2 144.4
+    // vs 143.4 us, C3 314 vs 307 us) — the setup, one workgroup per CU,
+    // reads the raw planes from HBM at ~2.3 TB/s, where step 1 streams them at full
+    // occupancy and the resident setup then re-reads its outputs from cache.
+    const char *fenv = getenv("NLSPN_RES_FIRST");
+    const ResFirstIn F{pred_init, conf, aff_raw, aff_bstride, off_out, gamma, kind};
+    if (fenv && fenv[0] == '1' &&
+        plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter, pred,
+                      workspace, B, H, W, kh, kw, T, flags, P, &F)) {
+        if (resident) *resident = P.ngroups | NLSPN_RESIDENT_FIRST;
+        if (ev) {  // no step-1 kernel: an empty interval
+            NLSPN_HIP_TRY(hipEventRecord(ev[0], s));
+            NLSPN_HIP_TRY(hipEventRecord(ev[1], s));
+        }
+        return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    }
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
                                    pred, workspace, B, H, W, kh, kw, T, flags, P);
     if (res) {  // step 1 zeroes the resident kernel's progress words
@@ -894,6 +951,10 @@ int nlspn_plan_launch(nlspn_plan_t plan, void *stream) {
         return plan->resident ? res_guard_after(s) : NLSPN_OK;
     }
     for (LaunchRec &r : plan->recs) {
+        if (!r.fn) {
+            NLSPN_HIP_TRY(hipMemsetAsync(r.zptr, 0, r.zbytes, s));
+            continue;
+        }
         void *args[] = {r.resident ? static_cast<void *>(&r.ra) : static_cast<void *>(&r.sa)};
         if (r.resident && (rc = res_guard_before(s))) return rc;
         NLSPN_HIP_TRY(hipLaunchKernel(r.fn, r.grid, r.block, args, r.lds, s));
@@ -1247,7 +1308,7 @@ int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, cons
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, e[0], e[1]) != hipSuccess) { rc = fail(NLSPN_EHIP, "hipEventElapsedTime"); break; }
         f += ms;
-        const int nrest = T < 2 ? 0 : (res ? 1 : T - 1);
+        const int nrest = T < 2 ? 0 : (res ? 1 : T - 1);  // res: one interval over every resident launch
         for (int k = 1; k <= nrest && rc == 0; ++k) {
             if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) != hipSuccess) rc = fail(NLSPN_EHIP, "hipEventElapsedTime");
             r += ms;

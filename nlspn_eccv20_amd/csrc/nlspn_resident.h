@@ -76,7 +76,17 @@ struct ResArgs {
     unsigned flags;
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
                         // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid),
-                        // 32 part 0 aborts at t = 2 (tests of the error reporting)
+                        // 32 part 0 aborts at its first wait (tests of the error reporting)
+    // flags kResFirst only: iteration 1 and the forward prologue run in this launch
+    // (no step-1 kernel).  `aff` / `conf` are then OUTPUTS written by the setup
+    // (aff_out, conf_out), and `off` holds the raw offsets.
+    const void *pinit;     // pred_init planes (H*W apart)
+    const void *conf_raw;  // raw confidence planes, or null (conf_prop off)
+    const void *aff_raw;   // raw affinity, K planes per item, batch stride aff_bs
+    long long aff_bs;      // elements
+    void *off_out;         // inserted offsets, 2(K+1) planes per item, contiguous, or null
+    const float *gamma;    // device, 1 float (aff_scale_const)
+    int kind;              // affinity kind (kAff*)
 };
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
@@ -105,6 +115,7 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 #endif
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
+constexpr unsigned kResFirst = 0x200u;            // ResArgs::flags: iteration 1 + the prologue in this launch
 
 // Band i of n over a length L owns [i*L/n, (i+1)*L/n); owner(v) is the largest i
 // with floor(i*L/n) <= v.
@@ -222,6 +233,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
     const bool off_ins = (a.flags & kResOffInserted) != 0;
+    const bool fused = (a.flags & kResFirst) != 0;  // iteration 1 (t = 0 below) and the prologue here
     const long long HW = (long long)H * W;
     const unsigned plane_bytes = (unsigned)HW * ES;
     gu32 *sync = (gu32 *)(a.sync);
@@ -245,11 +257,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     {
         float dv[4];
         float ak[K][4], aref[4];
-        const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
+        // fused: the raw K-plane affinity, normalised below (step 1's prologue)
+        const rsrc_t ra_ = fused ? make_rsrc(static_cast<const T *>(a.aff_raw) + (long long)b * a.aff_bs)
+                                 : make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, ak[k]);
+            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(fused ? k : (k < REF ? k : k + 1)) * plane_bytes, ak[k]);
             const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
@@ -257,20 +271,59 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) dv[e] = 0.f;
         if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
+        // conf (raw when fused) with the other loads: one round trip before the stores below
+        float cq[4] = {1.f, 1.f, 1.f, 1.f};
+        if (has_conf)
+            ResVec<T>::template load<0>(
+                make_rsrc(static_cast<const T *>(fused ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
+        if (fused) {
+            // step 1's prologue for the own quad (nlspn_step.h FIRST): the output-dict
+            // offsets (_off_insert, streamed: never re-read), the normalised affinity
+            // (_affinity_normalization + _aff_insert) and, below, conf'
+            if (active && a.off_out) {
+                const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
+                const float z[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
-            float s = 0.f;
+                for (int c = 0; c < K + 1; ++c) {
+                    const int k = c < REF ? c : c - 1;
+                    ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
+                    ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
+                }
+            }
+            normalize_taps<K, 4>(ak, aref, a.kind, *a.gamma);
+            if (active) {
+                const rsrc_t rao = make_rsrc(static_cast<T *>(const_cast<void *>(a.aff)) + (long long)b * (K + 1) * HW);
 #pragma unroll
-            for (int k = 0; k < K; ++k) s += ak[k][e];
-            aref[e] = 1.0f - s;
+                for (int c = 0; c < K + 1; ++c)
+                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, c == REF ? aref : ak[c < REF ? c : c - 1]);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < K; ++k) s += ak[k][e];
+                aref[e] = 1.0f - s;
+            }
         }
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
 #pragma unroll
         for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
         akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-        float cq[4] = {1.f, 1.f, 1.f, 1.f};
-        if (has_conf) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), vpix, 0u, cq);
+        if (has_conf && fused) {
+            // conf' = (1-m) conf + m (:341-348), stored write-through: other parts stage it
+            // from iteration 2 on (sc1 loads below), after this part's first publish
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float m = dv[e] > 0.f ? 1.f : 0.f;
+                cq[e] = preserve ? (1.0f - m) * cq[e] + m : cq[e];
+            }
+            if (active)
+                ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(const_cast<void *>(a.conf)) + b * HW), vpix, 0u, cq);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cq[e] = round_to<T>(cq[e]);  // as stored (the staging reloads it)
+        }
         akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
         akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
     }
@@ -279,8 +332,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (offsets are invariant, so once), when it fits the LDS cells allocated;
     // otherwise the part +- (RY rows, RXQ quads), and the rare taps outside it take
     // the general path.  Columns are whole quads plus PADX zero columns each side.
+    // The setup's barriers order LDS only (lds_barrier): global stores of the fused
+    // prologue stay in flight behind them.
     if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1 - 1; ctl[3] = 4 * c0; ctl[4] = 4 * c1 - 1; }
-    __syncthreads();
+    lds_barrier();
     if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
     const float Hf = (float)H, Wf = (float)W;
     {
@@ -305,7 +360,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         res_span_merge(ctl, active, mn, mx, cmn, cmx);
     }
-    __syncthreads();
+    lds_barrier();
     int rlo = ctl[1], rhi = ctl[2], wq0 = ctl[3] >> 2, wq1 = ctl[4] >> 2;  // >> 2: floor for negatives too
     if (rhi < rlo + 1) rhi = rlo + 1;  // at least two rows (the zero redirect reads a 2x2 footprint)
     if ((rhi - rlo + 1) * (4 * (wq1 - wq0 + 1) + 2 * PADX) > WC) {  // too large: fixed halo + general path
@@ -318,10 +373,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int ra = max(rlo, 0), rb = min(rhi, H - 1);      // in-image window rows
     const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
     const int wqn = qb - qa + 1;
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
-    __syncthreads();
+    lds_barrier();
     if (trace0 && tid == 0) trace0[2] = __builtin_amdgcn_s_memrealtime();
     // Classify every tap once:
     //  * invalid (outside (-1,H) x (-1,W), or NaN): the reference samples 0.  Its
@@ -358,7 +413,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         has_fb = has_fb && active;
         res_span_merge(ctl, has_fb, mn, mx, cmn, cmx);
     }
-    __syncthreads();
+    lds_barrier();
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
     // the parts this one reads: a rectangle of the image's part grid
     const int dy0 = res_owner(ctl[1], H, a.gy), dy1 = res_owner(ctl[2], H, a.gy);
@@ -408,7 +463,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
     const int lown = (y - rlo) * WW + x0 - 4 * wq0 + PADX;  // window cell of the own quad's first pixel
 
-    for (int t = 1; t < a.T; ++t) {
+    // Iteration t reads plane t-1 and writes plane t; fused: t = 0 is iteration 1, whose
+    // source is built from the raw inputs (p0 * conf', nlspn_step.h make_f<true>).  A part
+    // publishes epoch + t + 1 after iteration t, so iteration t waits for epoch + t; the
+    // first iteration of a launch waits for nothing (its source is an input).
+    const int t0 = fused ? 0 : 1;
+    for (int t = t0; t < a.T; ++t) {
         // The tap geometry depends only on the (invariant) coordinates, so the
         // compiler would hoist all 32 taps' weights and addresses out of this loop
         // and spill them; opaque register moves keep them per iteration (no code).
@@ -421,14 +481,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
         asm volatile("" : "+v"(tb));
 
-        unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
-                                                      ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
+        unsigned long long *trace = ((a.dbg & 8u) && t > 0) ? reinterpret_cast<unsigned long long *>(a.pred) +
+                                                                 ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
         // ---- wait until every part this one reads has finished iteration t-1
-        if (t >= 2 && tid < 64 && !(a.dbg & 1u)) {
+        if (t > t0 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
             bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
-            const unsigned need = a.epoch + (unsigned)(t - 1);
+            const unsigned need = a.epoch + (unsigned)t;
             for (int base = 0; base < ndep && !fail; base += 64) {
                 const int d = base + lane;
                 const int dy = d / ndx;
@@ -456,7 +516,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-        __syncthreads();  // also orders the previous iteration's LDS reads before the restaging
+        // also orders the previous iteration's LDS reads before the restaging.  A launch's
+        // first iteration needs LDS order only: the setup's output stores (fused prologue)
+        // keep draining under its staging and taps, until its publish
+        if (t > t0) __syncthreads();
+        else lds_barrier();
         if (ctl[0]) {  // aborted: NaN in every plane this part has not written, then exit
             if (active) {
                 const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
@@ -470,11 +534,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 
         // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
         // (written by other parts in this launch), conf' by plain loads (invariant)
-        const T *p_in = p_all + (size_t)(t - 1) * a.tstride + b * HW;
+        const bool first = t == 0;  // fused iteration 1: f = p0 * conf' from the raw inputs
+        const T *p_in = first ? static_cast<const T *>(a.pinit) + b * HW : p_all + (size_t)(t - 1) * a.tstride + b * HW;
         const rsrc_t rp = make_rsrc(p_in);
-        // t >= 2: the own quads are in the window already (written back below), so
-        // only the other parts' quads are loaded
-        const bool rim = t >= 2;
+        // after a launch's first iteration the own quads are in the window already
+        // (written back below), so only the other parts' quads are loaded
+        const bool rim = t > t0;
         const int nsq_it = (a.dbg & 2u) ? 0 : (rim ? nrest : nall);
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
@@ -495,8 +560,31 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 sl[s] = (r - rlo) * WW + 4 * (c - wq0) + PADX;  // window cell, % 4 == 0
                 if (k < nsq_it) {
                     const unsigned go = (unsigned)(r * W + 4 * c) * ES;
-                    ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
-                    if (has_conf) ResVec<T>::template load<0>(rcg, go, 0u, cv[s]);
+                    if (first) {  // inputs of the launch: plain loads; p0 and conf' built below
+                        ResVec<T>::template load<0>(rp, go, 0u, sv[s]);
+                        if (has_conf)
+                            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf_raw) + b * HW), go, 0u, cv[s]);
+                        if (preserve) {
+                            float dq[4];
+                            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), go, 0u, dq);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {  // make_f<true> (nlspn_step.h), conf' folded into cv
+                                const float m = dq[e] > 0.f ? 1.f : 0.f;
+                                sv[s][e] = (1.0f - m) * sv[s][e] + m * dq[e];
+                                if (has_conf) cv[s][e] = (1.0f - m) * cv[s][e] + m;
+                            }
+                        }
+                        if (clip) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) sv[s][e] = clamp0(sv[s][e]);
+                        }
+                    } else {
+                        ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
+                        if (has_conf) {  // conf' written in this launch (fused): write-through hand-off
+                            if (fused) ResVec<T>::template load<kSc1>(rcg, go, 0u, cv[s]);
+                            else ResVec<T>::template load<0>(rcg, go, 0u, cv[s]);
+                        }
+                    }
                 }
             }
 #pragma unroll
@@ -591,8 +679,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                     c4[u] = 0.f;
                                     if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
                                         const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                        const float pv = ResVec<T>::template load1<kSc1>(rp, qo, 0u);
-                                        c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                                        if (first) {  // fetch_f<FIRST> of nlspn_step.h
+                                            const float pv = ResVec<T>::template load1<0>(rp, qo, 0u);
+                                            const float cr = has_conf ? ResVec<T>::template load1<0>(
+                                                make_rsrc(static_cast<const T *>(a.conf_raw) + b * HW), qo, 0u) : 1.f;
+                                            const float dr = preserve ? ResVec<T>::template load1<0>(
+                                                make_rsrc(static_cast<const T *>(a.dep) + b * HW), qo, 0u) : 0.f;
+                                            c4[u] = make_f<true>(pv, cr, dr, has_conf, preserve, clip);
+                                        } else {
+                                            const float pv = ResVec<T>::template load1<kSc1>(rp, qo, 0u);
+                                            const float cg = !has_conf ? 1.f
+                                                             : fused ? ResVec<T>::template load1<kSc1>(rcg, qo, 0u)
+                                                                     : ResVec<T>::template load1<0>(rcg, qo, 0u);
+                                            c4[u] = has_conf ? pv * cg : pv;
+                                        }
                                     }
                                 }
                                 v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
@@ -630,7 +730,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         __syncthreads();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0)
-            __hip_atomic_store(&sync[1 + blockIdx.x], a.epoch + (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[1 + blockIdx.x], a.epoch + (unsigned)t + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (ES == 2) {
+            // fused, fp16: iteration 1 used the normalised affinity unrounded (as step 1
+            // does); the later iterations use it as stored (aff_out), reference weight
+            // 1 - sum of the stored taps (the step kernel's non-first arithmetic)
+            if (first && active) {
+                float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    float4 v = akl[k];
+                    v.x = round_to<T>(v.x); v.y = round_to<T>(v.y); v.z = round_to<T>(v.z); v.w = round_to<T>(v.w);
+                    akl[k] = v;
+                    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
+                }
+                akl[K] = make_float4(1.0f - s4[0], 1.0f - s4[1], 1.0f - s4[2], 1.0f - s4[3]);
+            }
+        }
         // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
         // this iteration is done: the barrier above), as the next staging would load it
         if (t < a.T - 1 && active && !(a.dbg & 2u)) {

@@ -1,10 +1,11 @@
-"""GPU: the resident propagation kernel (iterations 2..T in one launch, invariant
-planes on chip, per-workgroup progress words) against the per-iteration launches
-and the oracle.
+"""GPU: the resident propagation kernel (iterations 2..T in one launch per image
+group after a step-1 launch — or, NLSPN_RES_FIRST=1, the prologue and iterations
+1..T in the launches — invariant planes on chip, per-workgroup progress words)
+against the per-iteration launches and the oracle.
 
-Bar: BIT-EXACT against the T-1 per-iteration launches (both issue the same IEEE
-sequence per pixel; only the schedule and the hand-off differ), every one of the
-T pred_inter planes, and no abort raised.  Exercised where hand-offs are most
+Bar: BIT-EXACT against step 1 + the T-1 per-iteration launches (all forms issue the
+same IEEE sequence per pixel; only the schedule and the hand-off differ), every one
+of the T pred_inter planes and the prologue's outputs, and no abort raised.  Exercised where hand-offs are most
 fragile: long-range offsets (dependency ranges over many parts, taps beyond the
 LDS window), tiny parts, repeated graph replays (a stale read shows up as a
 replay that differs), fp16 storage, and every flag combination.
@@ -35,18 +36,18 @@ def resident_config(B, H, W, dtype=0, conf=True, T=18):
 
 
 class _env:
-    def __init__(self, value):
-        self.value = value
+    def __init__(self, value, name="NLSPN_RESIDENT"):
+        self.value, self.name = value, name
 
     def __enter__(self):
-        self.old = os.environ.get("NLSPN_RESIDENT")
-        os.environ["NLSPN_RESIDENT"] = self.value
+        self.old = os.environ.get(self.name)
+        os.environ[self.name] = self.value
 
     def __exit__(self, *a):
         if self.old is None:
-            os.environ.pop("NLSPN_RESIDENT", None)
+            os.environ.pop(self.name, None)
         else:
-            os.environ["NLSPN_RESIDENT"] = self.old
+            os.environ[self.name] = self.old
 
 
 def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=0.05):
@@ -57,14 +58,21 @@ def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=
 
 
 def _both(inp, T=18, **kw):
+    """(resident, steps): the default resident form (behind a step-1 launch), checked
+    here against the resident form with iteration 1 inside the launches, and the step form."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
+        with _env("1", "NLSPN_RES_FIRST"):
+            c = propagate(*inp, prop_time=T, **kw)
     with _env("0"):
         b = propagate(*inp, prop_time=T, **kw)
     torch.cuda.synchronize()
     for k in ("aff", "offset", "confidence"):  # the prologue's output-dict tensors
         if a[k] is not None or b[k] is not None:
             assert _bits_equal(a[k], b[k]), k
+            assert _bits_equal(c[k], b[k]), k
+    assert _bits_equal(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
+    assert _bits_equal(a["pred"], c["pred"])
     return a, b
 
 
@@ -176,20 +184,26 @@ def test_resident_vs_oracle_c2(oracle):
 
 def test_time_propagate_reports_resident():
     inp, _ = _inputs(8, 228, 304)
-    os.environ["NLSPN_RESIDENT"] = "1"
-    plan = PropagationPlan(*inp, prop_time=18)
-    o = plan.outputs
-    first, rest, res = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
     pi, dep, conf, aff, off, g = inp
-    _lib.check(_lib.get().nlspn_time_propagate(
-        0, pi.data_ptr(), dep.data_ptr(), conf.data_ptr(), aff.data_ptr(), aff.stride(0), off.data_ptr(),
-        off.stride(0), g.data_ptr(), o["pred_inter"].data_ptr(), o["pred"].data_ptr(), o["aff"].data_ptr(),
-        o["offset"].data_ptr(), o["confidence"].data_ptr(), o["workspace"].data_ptr(), 8, 228, 304, 3, 3, 18, 3,
-        _lib.PRESERVE_INPUT, 3, torch.cuda.current_stream().cuda_stream, ctypes.byref(first), ctypes.byref(rest),
-        ctypes.byref(res)))
-    os.environ.pop("NLSPN_RESIDENT", None)
-    assert res.value == 1 and first.value > 0 and rest.value > 0  # one resident launch (one image group)
-    plan.close()
+
+    def timed(o):
+        first, rest, res = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        _lib.check(_lib.get().nlspn_time_propagate(
+            0, pi.data_ptr(), dep.data_ptr(), conf.data_ptr(), aff.data_ptr(), aff.stride(0), off.data_ptr(),
+            off.stride(0), g.data_ptr(), o["pred_inter"].data_ptr(), o["pred"].data_ptr(), o["aff"].data_ptr(),
+            o["offset"].data_ptr(), o["confidence"].data_ptr(), o["workspace"].data_ptr(), 8, 228, 304, 3, 3, 18, 3,
+            _lib.PRESERVE_INPUT, 3, torch.cuda.current_stream().cuda_stream, ctypes.byref(first),
+            ctypes.byref(rest), ctypes.byref(res)))
+        return first.value, rest.value, res.value
+
+    with _env("1"):
+        plan = PropagationPlan(*inp, prop_time=18)
+        first, rest, res = timed(plan.outputs)
+        assert res == 1 and first > 0 and rest > 0  # one resident launch (one image group) behind step 1
+        with _env("1", "NLSPN_RES_FIRST"):  # iteration 1 inside the resident launch: no step-1 kernel
+            first, rest, res = timed(plan.outputs)
+        assert res == 1 | _lib.RESIDENT_FIRST and first >= 0 and rest > 0
+        plan.close()
 
 
 def test_c3_resident_vs_oracle_and_replays(oracle):
