@@ -30,7 +30,7 @@
 // MI355X_MICROARCH.md § inter-workgroup visibility):
 //   producer: every p_t store is `sc1` (write-through), every wave drains
 //             (s_waitcnt vmcnt(0)), workgroup barrier, ONE lane stores its
-//             progress word = epoch + t (relaxed, agent scope = sc1 store);
+//             progress word = epoch + t + 1 (relaxed, agent scope = sc1 store);
 //   consumer: ONE wave polls the words it depends on (relaxed sc1 loads),
 //             workgroup barrier, then EVERY load of a pred_inter plane is an
 //             `sc1` load (no acquire fence needed, L1 bypassed).
@@ -38,7 +38,7 @@
 // Every plane t is written once, so there is no write-after-read hazard and a
 // fast part may run ahead of parts that do not feed it.  Image groups run as
 // back-to-back launches on one stream; group k's progress values start at
-// epoch = k * T, above everything group k-1 left in the words, so the words are
+// epoch = k * (T + 1), above everything group k-1 left in the words, so the words are
 // zeroed once per section (by step 1).
 //
 // Residency: G = B * gy * gx workgroups, at most one per CU (the dynamic LDS
@@ -72,7 +72,7 @@ struct ResArgs {
     int B, H, W, T;     // B: images of this launch
     int gy, gx;         // parts per image: gy row bands x gx quad-column bands
     int win_cells;      // LDS cells per copy of the f window: res_win_cells(blockDim.x)
-    unsigned epoch;     // progress-word base of this launch (k * T for image group k)
+    unsigned epoch;     // progress-word base of this launch (k * (T + 1) for image group k)
     unsigned flags;
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
                         // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid),
