@@ -13,6 +13,7 @@ with a torch-facing mirror of the reference interface:
   dcn                           — `DCN`-compatible module (seam 2)
   model.NLSPNModel              — the whole reference model (seam 1), encoder/decoder on MIOpen
   model.SectionGraph            — its propagation section (GRU mode included) as one hipGraph
+  replay                        — the reference's summary dumps (offset.npy / aff.npy / gamma.npy) re-run
 """
 from .model import NLSPNModel, SectionGraph
 from .propagation import (NLSPNPropagation, PropagationPlan, affinity_normalization, kernel_geometry,
