@@ -176,16 +176,16 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
         # 2K offsets); writes aff (K+1), offsets (2(K+1)), conf', pred_inter[0..T-1], pred
         comp_planes = (3 * K + 3) + (3 * K + 5 + T)
         alg_iters = T
-        kdesc = (f"{kname} (prologue + iterations 1..{T}, invariant planes on chip: {resident} launch(es), one "
-                 f"per image group; kernel_ms_mean spans them all)")
+        kdesc = (f"{kname} (prologue + iterations 1..{T}, invariant planes on chip: {resident} launch(es), the "
+                 f"full image groups in turn inside one; kernel_ms_mean spans them all)")
     elif resident:
         kname, kmean = "prop_resident_kernel", rest_ms
         # reads: K normalised affinities (tap K/2 is recomputed), 2K offsets, conf', dep, p_1;
         # writes: pred_inter[1..T-1] and pred
         comp_planes = (K + 2 * K + 2 + 1) + (T - 1 + 1)
         alg_iters = T - 1
-        kdesc = (f"{kname} (iterations 2..{T}, invariant planes on chip: {resident} launch(es), one per image "
-                 f"group; kernel_ms_mean spans them all)")
+        kdesc = (f"{kname} (iterations 2..{T}, invariant planes on chip: {resident} launch(es), the full "
+                 f"image groups in turn inside one; kernel_ms_mean spans them all)")
     else:
         kname, kmean = "prop_step_kernel", rest_ms / max(1, T - 1)
         comp_planes = 4 + 3 * K  # p_in, conf', dep, K aff, 2K offsets read; p_out written
@@ -197,7 +197,7 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
     sec = ((3 * K + 3) + (T + 3 * K + 5)) * plane
     traffic = pmc_traffic(name, kname)
     if traffic and resident:
-        traffic *= resident  # per launch -> the section's iterations 2..T (one launch per image group)
+        traffic *= resident  # per launch -> the section's iterations 2..T (all launches)
     return {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kdesc,

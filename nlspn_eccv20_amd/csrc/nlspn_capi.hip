@@ -439,6 +439,23 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
         }
     }
     P.first = F != nullptr;
+    // The full image groups run in turn inside ONE launch (ResArgs::ngroups): no launch
+    // boundary between them, so a part sets up its next group while others finish the
+    // current one.  A partial last group keeps a launch of its own (its grid differs).
+    // NLSPN_RES_MERGE=0 (A/B) or a trace (dbg 8, one record per part) keeps one launch
+    // per group.
+    const char *menv = getenv("NLSPN_RES_MERGE");
+    const int nfull = B / S.Bg;
+    if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
+        P.a[0].ngroups = nfull;
+        int n = 1;
+        if (ng > nfull) {  // the partial group, launched after the merged one
+            P.a[1] = P.a[ng - 1];
+            P.grid[1] = P.grid[ng - 1];
+            n = 2;
+        }
+        P.ngroups = n;
+    }
     return true;
 }
 

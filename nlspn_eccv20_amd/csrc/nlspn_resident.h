@@ -36,10 +36,11 @@
 //             `sc1` load (no acquire fence needed, L1 bypassed).
 // Loads of bytes not written in this launch (conf', invariants) are plain.
 // Every plane t is written once, so there is no write-after-read hazard and a
-// fast part may run ahead of parts that do not feed it.  Image groups run as
-// back-to-back launches on one stream; group k's progress values start at
-// epoch = k * (T + 1), above everything group k-1 left in the words, so the words are
-// zeroed once per section (by step 1).
+// fast part may run ahead of parts that do not feed it.  Image groups run in turn
+// inside one launch (ResArgs::ngroups; a part sets up group k + 1 as soon as it has
+// published its last iteration of group k, while other parts still finish group k);
+// group k's progress values start at epoch = k * (T + 1), above everything group k-1
+// left in the words, so the words are zeroed once per section (by step 1).
 //
 // Residency: G = B * gy * gx workgroups, at most one per CU (the dynamic LDS
 // request exceeds half a CU's LDS) and G <= CU count, so the whole grid is
@@ -87,6 +88,11 @@ struct ResArgs {
     void *off_out;         // inserted offsets, 2(K+1) planes per item, contiguous, or null
     const float *gamma;    // device, 1 float (aff_scale_const)
     int kind;              // affinity kind (kAff*)
+    // image groups this launch runs in turn (0 or 1: one).  Group g is images
+    // g*B .. g*B + B - 1 from the base pointers above, with progress values from
+    // epoch + g (T + 1): a part starts group g + 1 as soon as it has published its last
+    // iteration of group g, with no launch boundary between the groups.
+    int ngroups;
 };
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
@@ -215,6 +221,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // offset from ONE address register.
     float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
 
+    gu32 *sync = (gu32 *)(a.sync);
+    const int ngroups = a.ngroups > 1 ? a.ngroups : 1;
+    // ---- image groups in turn: every plane pointer below is offset by the image b
+    for (int grp = 0; grp < ngroups; ++grp) {
+    unsigned bid = blockIdx.x;
+    asm volatile("" : "+s"(bid));
     const int H = a.H, W = a.W, W4 = W / 4;
     // Part numbering: logical index L = b * (gy*gx) + j, dealt to the XCDs in contiguous
     // runs (xcd_remap), so the parts of an image — and neighbouring parts — share an
@@ -222,8 +234,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // in bands of 32 parts; C1: bands of 32 parts).  Speed only: progress words are
     // indexed by blockIdx, and a consumer maps the parts it reads back (xcd_unmap).
     const int nparts = a.gy * a.gx, G = a.B * nparts;
-    const int L = xcd_remap((int)blockIdx.x, G);
-    const int b = L / nparts, j = L - b * nparts;
+    // (bid: blockIdx behind an opaque move, so that nothing derived from it is hoisted
+    // out of the group loop and held in registers across the groups)
+    const int L = xcd_remap((int)bid, G);
+    const int bl = L / nparts, j = L - bl * nparts;  // image of the group, part of the image
     const int py = j / a.gx, px = j % a.gx;
     const int r0 = (int)((long long)py * H / a.gy), r1 = (int)((long long)(py + 1) * H / a.gy);    // own rows
     const int c0 = (int)((long long)px * W4 / a.gx), c1 = (int)((long long)(px + 1) * W4 / a.gx);  // own quad cols
@@ -236,7 +250,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const bool fused = (a.flags & kResFirst) != 0;  // iteration 1 (t = 0 below) and the prologue here
     const long long HW = (long long)H * W;
     const unsigned plane_bytes = (unsigned)HW * ES;
-    gu32 *sync = (gu32 *)(a.sync);
+    const int b = bl + grp * a.B;
+    const unsigned epoch = a.epoch + (unsigned)grp * (unsigned)(a.T + 1);
 
     // ---- own quad and its invariants.  Taps are held as their sample coordinates
     // (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw), the reference's own
@@ -488,7 +503,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (t > t0 && tid < 64 && !(a.dbg & 1u)) {
             unsigned spins = 0;
             bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
-            const unsigned need = a.epoch + (unsigned)t;
+            const unsigned need = epoch + (unsigned)t;
             for (int base = 0; base < ndep && !fail; base += 64) {
                 const int d = base + lane;
                 const int dy = d / ndx;
@@ -497,7 +512,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 // so a spin is ONE memory round trip (a separate abort load per spin, issued
                 // after the ballot, doubled the poll period)
                 const bool spare = base + 64 > ndep;
-                gu32 *wp = d < ndep ? &sync[1 + xcd_unmap(b * nparts + jj, G)] : &sync[0];
+                gu32 *wp = d < ndep ? &sync[1 + xcd_unmap(bl * nparts + jj, G)] : &sync[0];
                 for (;;) {
                     const unsigned v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (__all(d >= ndep || v >= need)) break;
@@ -521,12 +536,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // keep draining under its staging and taps, until its publish
         if (t > t0) __syncthreads();
         else lds_barrier();
-        if (ctl[0]) {  // aborted: NaN in every plane this part has not written, then exit
+        if (ctl[0]) {  // aborted: NaN in every plane this part has not written (this group's
+                       // remaining iterations, every later group's), then exit
             if (active) {
                 const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
-                for (int tt = t; tt < a.T; ++tt)
-                    ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b * HW), vpix, 0u, qn);
-                ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, qn);
+                for (int g2 = grp; g2 < ngroups; ++g2) {
+                    const int b2 = bl + g2 * a.B;
+                    for (int tt = g2 == grp ? t : t0; tt < a.T; ++tt)
+                        ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u,
+                                                     qn);
+                    ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
+                }
             }
             return;
         }
@@ -730,7 +750,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         __syncthreads();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0)
-            __hip_atomic_store(&sync[1 + blockIdx.x], a.epoch + (unsigned)t + 1u, __ATOMIC_RELAXED,
+            __hip_atomic_store(&sync[1 + blockIdx.x], epoch + (unsigned)t + 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (ES == 2) {
             // fused, fp16: iteration 1 used the normalised affinity unrounded (as step 1
@@ -762,6 +782,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             fwinB[lown + 2] = f.w;
         }
     }
+    }  // image groups
 }
 
 }  // namespace nlspn

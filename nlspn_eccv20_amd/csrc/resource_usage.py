@@ -43,19 +43,21 @@ def load_build(build_dir: str = BUILD_DIR) -> dict:
     return rows
 
 
-def loop_scratch(asm: str, name: str) -> dict:
+def loop_scratch(asm: str, name: str, min_depth: int = 1) -> dict:
     """Scratch (spill) instructions of kernel `name` in device assembly text (hipcc -S
-    --cuda-device-only), split into those inside a loop (LLVM's `; in Loop:` block
-    comments) and the rest: {"loop": [...], "other": [...]} of instruction lines."""
+    --cuda-device-only), split into those inside a loop nest at least `min_depth` deep
+    (LLVM's `; in Loop: ... Depth=N` block comments) and the rest: {"loop": [...],
+    "other": [...]} of instruction lines."""
     i = asm.index(name + ":")
     body = asm[i:asm.index(".Lfunc_end", i)]
-    out, in_loop = {"loop": [], "other": []}, False
+    out, depth = {"loop": [], "other": []}, 0
     for line in body.splitlines():
-        m = re.match(r"^\.LBB\d+_\d+:(.*)", line)
+        m = re.match(r"^(?:\.LBB\d+_\d+:|; %bb\.\d+:)(.*)", line)
         if m:
-            in_loop = "in Loop:" in m.group(1)
+            d = re.search(r"in Loop:.*Depth=(\d+)", m.group(1))
+            depth = int(d.group(1)) if d else 0
         elif "scratch_" in line:
-            out["loop" if in_loop else "other"].append(line.strip())
+            out["loop" if depth >= min_depth else "other"].append(line.strip())
     return out
 
 

@@ -207,9 +207,9 @@ def test_time_propagate_reports_resident():
 
 
 def test_c3_resident_vs_oracle_and_replays(oracle):
-    """C3 (KITTI B=4) runs iterations 2..T as two back-to-back resident launches of two
-    images each (progress words carried across them by epoch): against the oracle at the
-    north-star bar, and stable over plan replays."""
+    """C3 (KITTI B=4) runs iterations 2..T as two image groups of two images each, in
+    turn inside one resident launch (progress words carried across them by epoch):
+    against the oracle at the north-star bar, and stable over plan replays."""
     inp, s = _inputs(4, 240, 1216, seed=7240)
     with _env("1"):
         plan = PropagationPlan(*inp, prop_time=18)
