@@ -34,9 +34,6 @@ from . import propagation as P
 
 __all__ = ["SummaryDump", "load_dump", "save_dump", "replay"]
 
-_FILES = ("offset.npy", "aff.npy", "gamma.npy")
-
-
 @dataclass
 class SummaryDump:
     """The planes of one summary dump (float32, as the reference saves them)."""
@@ -141,7 +138,9 @@ def replay(dump: SummaryDump, pred_init, dep, confidence=None, *, prop_time: int
     offset, aff, gamma, confidence (blended) — and pred_inter_tensor."""
     B, H, W = dump.shape
     kh, kw = dump.kernel
-    K = kh * kw - 1
+    T = int(prop_time)
+    if T < 1:
+        raise ValueError(f"prop_time must be >= 1, got {prop_time}")
     dev = torch.device(device)
     if dev.type != "cuda":
         raise RuntimeError("replay runs on the HIP path: device must be a CUDA (HIP) device")
@@ -155,7 +154,6 @@ def replay(dump: SummaryDump, pred_init, dep, confidence=None, *, prop_time: int
         raise RuntimeError("preserve_input requires dep")
     aff = _dev(dump.aff, dev, dtype)
     off = _dev(dump.offset, dev, dtype)
-    T = int(prop_time)
 
     p0 = p
     if preserve_input:  # :328-334, :343-345, in the reference's operation order

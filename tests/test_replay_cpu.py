@@ -80,3 +80,11 @@ def test_replay_requires_the_hip_device(tmp_path):
                               "gamma": torch.from_numpy(z["gamma"])})
     with pytest.raises(RuntimeError, match="HIP"):
         replay(load_dump(str(tmp_path)), z["pred_init"], z["dep"], z["conf"], device="cpu")
+
+
+def test_replay_rejects_bad_prop_time(tmp_path):
+    z = load_golden("loop_tgass_preserve")
+    save_dump(str(tmp_path), {"aff": torch.from_numpy(z["aff"]), "offset": None,
+                              "gamma": torch.from_numpy(z["gamma"])})
+    with pytest.raises(ValueError, match="prop_time"):
+        replay(load_dump(str(tmp_path)), z["pred_init"], z["dep"], z["conf"], prop_time=0, device="cuda")
