@@ -25,9 +25,11 @@
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
 #define NLSPN_RES_EXTERN(T)                                                       \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128>(ResArgs);
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>(ResArgs);    \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
 NLSPN_RES_EXTERN(float)
 NLSPN_RES_EXTERN(__half)
 // defined in nlspn_kern_heads.hip
@@ -297,6 +299,7 @@ constexpr int kResMaxGroups = 64;  // image groups (back-to-back resident launch
 
 struct ResPlan {
     const void *fn = nullptr;
+    const void *fn_merged = nullptr;  // launch 0's kernel when it runs several image groups
     unsigned block = 0;
     size_t lds = 0, sync_bytes = 0;
     int ngroups = 0;
@@ -306,10 +309,13 @@ struct ResPlan {
 };
 
 template <typename T>
-const void *res_fn(long long nt) {
-    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576>);
-    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128>);
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0>);
+const void *res_fn(long long nt, bool groups) {
+    if (groups)
+        return nt == 576 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>)
+                         : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>);
+    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>);
+    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>);
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>);
 }
 
 // The part grid of a resident launch: Bg images per launch, each cut into gy row
@@ -404,7 +410,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if ((G + 1) * 4 > kSyncBytes) return false;
     const size_t lds = 4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt;
     if (lds > (size_t)kResLds || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt) : res_fn<__half>(S.nt);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false) : res_fn<__half>(S.nt, false);
     P.block = (unsigned)S.nt;
     P.lds = lds;
     P.sync_bytes = ((G + 1) * 4 + 15) / 16 * 16;
@@ -448,6 +454,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const int nfull = B / S.Bg;
     if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
         P.a[0].ngroups = nfull;
+        // the group-loop build for the merged launch; a partial last group keeps the other
+        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true) : res_fn<__half>(S.nt, true);
         int n = 1;
         if (ng > nfull) {  // the partial group, launched after the merged one
             P.a[1] = P.a[ng - 1];
@@ -464,6 +472,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
 // e0 is recorded at the start of the first group's launch, e1 at the end of the last.
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
+    if (P.fn_merged)
+        NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn_merged, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
     if (P.first) {
         if (g_rec) {
             LaunchRec z{};
@@ -474,16 +484,17 @@ int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent
         NLSPN_HIP_TRY(hipMemsetAsync(P.a[0].sync, 0, P.sync_bytes, s));
     }
     for (int k = 0; k < P.ngroups; ++k) {
+        const void *fn = k == 0 && P.fn_merged ? P.fn_merged : P.fn;
         if (g_rec)
-            g_rec->push_back(LaunchRec{P.fn, dim3(P.grid[k]), dim3(P.block), P.lds, true, StepArgs{}, P.a[k]});
+            g_rec->push_back(LaunchRec{fn, dim3(P.grid[k]), dim3(P.block), P.lds, true, StepArgs{}, P.a[k]});
         int rc = res_guard_before(s);
         if (rc) return rc;
         void *args[] = {&P.a[k]};
         hipEvent_t s0 = k == 0 ? e0 : nullptr, s1 = k == P.ngroups - 1 ? e1 : nullptr;
         if (s0 || s1)
-            NLSPN_HIP_TRY(hipExtLaunchKernel(P.fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s, s0, s1, 0));
+            NLSPN_HIP_TRY(hipExtLaunchKernel(fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s, s0, s1, 0));
         else
-            NLSPN_HIP_TRY(hipLaunchKernel(P.fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s));
+            NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(P.grid[k]), dim3(P.block), args, P.lds, s));
         if ((rc = check_launch("nlspn_propagate resident"))) return rc;
         if ((rc = res_guard_after(s))) return rc;
     }

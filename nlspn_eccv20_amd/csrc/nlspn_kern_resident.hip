@@ -7,11 +7,14 @@
 namespace nlspn {
 // NTC: compile-time thread counts of the shapes the bench configs plan (C2 NYU B=8:
 // 576; one NYU image, C1: 128), so the LDS row addresses fold into immediates;
-// 0 = any other shape (thread count read at run time).
-#define NLSPN_RES_INST(T)                                                  \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0>(ResArgs);   \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128>(ResArgs);
+// 0 = any other shape (thread count read at run time).  GROUPS = true: several image
+// groups in turn in one launch (C3 KITTI B=4: 576 threads; others: run-time count).
+#define NLSPN_RES_INST(T)                                                                \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>(ResArgs);    \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
 NLSPN_RES_INST(float)
 NLSPN_RES_INST(__half)
 }  // namespace nlspn

@@ -199,7 +199,9 @@ template <> struct ResVec<__half> {
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
 // MAXNT = launch bound (threads), SMAX = staging quads per thread per round.
 // NTC = the thread count as a compile-time constant (0: blockDim.x at run time).
-template <typename T, int MAXNT, int SMAX, int NTC>
+// GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
+// folds away, and with it the setup spill slots it costs).
+template <typename T, int MAXNT, int SMAX, int NTC, bool GROUPS>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RXQ = kResRXQ, PADX = kResPadX;
     constexpr unsigned ES = sizeof(T);
@@ -222,7 +224,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
 
     gu32 *sync = (gu32 *)(a.sync);
-    const int ngroups = a.ngroups > 1 ? a.ngroups : 1;
+    const int ngroups = GROUPS && a.ngroups > 1 ? a.ngroups : 1;
     // ---- image groups in turn: every plane pointer below is offset by the image b
     for (int grp = 0; grp < ngroups; ++grp) {
     unsigned bid = blockIdx.x;
