@@ -95,6 +95,8 @@ struct ResArgs {
     int ngroups;
 };
 
+typedef const __attribute__((address_space(4))) ResArgs ResArgsK;  // the kernarg segment's ResArgs
+
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
 #ifndef NLSPN_RES_SMAX
 #define NLSPN_RES_SMAX 1
@@ -229,6 +231,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     for (int grp = 0; grp < ngroups; ++grp) {
     unsigned bid = blockIdx.x;
     asm volatile("" : "+s"(bid));
+    // GROUPS: the arguments are re-read per group through an opaque kernarg-segment
+    // pointer, so their loads are not hoisted out of the group loop and held (spilled)
+    // across every iteration of every group
+    ResArgsK *akp = (ResArgsK *)__builtin_amdgcn_kernarg_segment_ptr();
+    if constexpr (GROUPS) asm volatile("" : "+s"(akp));
+    const ResArgsK &a = *akp;
     const int H = a.H, W = a.W, W4 = W / 4;
     // Part numbering: logical index L = b * (gy*gx) + j, dealt to the XCDs in contiguous
     // runs (xcd_remap), so the parts of an image — and neighbouring parts — share an
