@@ -226,6 +226,52 @@ def test_c3_resident_vs_oracle_and_replays(oracle):
         plan.close()
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_merged_groups_and_partial_group_bit_exact(dtype):
+    """KITTI B=5: image groups of two, so the two full groups run in turn inside ONE
+    launch (the GROUPS build) and the partial fifth image in a launch of its own —
+    bit-exact against the step launches, against iteration 1 inside the launches, and
+    against one launch per group (NLSPN_RES_MERGE=0)."""
+    inp, _ = _inputs(5, 240, 1216, seed=11, dtype=dtype)
+    a, b = _both(inp)
+    assert _bits_equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
+    assert _bits_equal(a["pred"], b["pred"])
+    with _env("1"), _env("0", "NLSPN_RES_MERGE"):
+        c = propagate(*inp, prop_time=18)
+    torch.cuda.synchronize()
+    assert _bits_equal(a["pred_inter_tensor"], c["pred_inter_tensor"])
+    _lib.check_resident()
+
+
+def test_merged_launch_abort_raises_and_poisons():
+    """An abort inside a merged (two-group) launch: RuntimeError, and NaN — not stale or
+    plausible depths — in the planes the aborted part never wrote, for every group."""
+    inp, _ = _inputs(4, 240, 1216, seed=12)
+    old = os.environ.get("NLSPN_RES_DBG")
+    os.environ["NLSPN_RES_DBG"] = "32"
+    try:
+        with _env("1"):
+            plan = PropagationPlan(*inp, prop_time=18)
+        o = plan.replay()
+        with pytest.raises(RuntimeError, match="aborted"):
+            plan.check()
+        p = o["pred_inter_tensor"]
+        assert torch.isnan(p[1:, 0]).any()  # group 0: the aborting part's own image
+        assert torch.isnan(p[1:, 2]).any() and torch.isnan(o["pred"][2]).any()  # its quads of group 1
+        plan.close()
+    finally:
+        if old is None:
+            os.environ.pop("NLSPN_RES_DBG", None)
+        else:
+            os.environ["NLSPN_RES_DBG"] = old
+    _lib.check_resident()
+    with _env("1"):
+        o = propagate(*inp, prop_time=18)
+    torch.cuda.synchronize()
+    _lib.check_resident()
+    assert not torch.isnan(o["pred"]).any()
+
+
 def test_two_plans_on_two_streams_bit_exact():
     """Two resident plans replayed concurrently on two streams of one device: the
     library serialises resident launches across streams (co-residency), so every
