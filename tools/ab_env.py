@@ -3,7 +3,7 @@ environment setting read at plan creation (default: NLSPN_RES_FIRST=1, the secti
 first iteration inside the resident launches, vs step 1 as its own launch).  Both
 plans replay on the same inputs in alternating rounds of 20, so box-to-box and drift
 noise cancel; prints the median per-section time of each per config (JSON).
-usage: python tools/ab_res_first.py [--rounds 15] [--env NAME=VALUE] [--configs nyu,kitti]"""
+usage: python tools/ab_env.py [--rounds 15] [--env NAME=VALUE] [--configs nyu,kitti]"""
 import json
 import os
 import sys
