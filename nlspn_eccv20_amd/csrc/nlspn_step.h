@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) asum[p] = 0.f;
     const float Hf = (float)H, Wf = (float)W;
+    const float yb_f = (float)(y - PH), xb_f = (float)(xb - PW);  // |values| < 2^24: exact
     constexpr int NFB = (K * PX + 31) / 32;
     uint32_t fb[NFB];
 #pragma unroll
@@ -295,14 +296,20 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
                 continue;
             }
             // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
-            const float h_im = (float)(y - PH + i) + tdh[p];
-            const float w_im = (float)(xb + p - PW + j) + tdw[p];
+            // the tap's base coordinates as exact float sums of small integers (one add per
+            // tap instead of an integer add and a convert): the same values as
+            // (float)(y - PH + i) and (float)(xb + p - PW + j)
+            const float h_im = (yb_f + (float)i) + tdh[p];
+            const float w_im = (xb_f + (float)(p + j)) + tdw[p];
             float v = 0.f;
             if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                // inside (-1, H) x (-1, W): floor fits an int, and (float)h_low == fh, so
+                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36)
+                const float fh = floorf(h_im), fw = floorf(w_im);
+                const int h_low = (int)fh, w_low = (int)fw;
                 const int ry = h_low - wy0, rx = w_low - wx0;
                 if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
-                    const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                    const float lh = h_im - fh, lw = w_im - fw;
                     const float hh = 1.f - lh, hw = 1.f - lw;
                     const float *s = &win[ry * WW + rx];
                     const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
