@@ -90,8 +90,8 @@ def get() -> ctypes.CDLL:
                 "There is no CPU fallback for the propagation hot path.")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if not hasattr(lib, name) and os.environ.get("NLSPN_LIB_PATH") and name == "nlspn_resident_status":
-                continue  # A/B against an older build (ABI 2) without the status word
+            if not hasattr(lib, name) and os.environ.get("NLSPN_LIB_PATH"):
+                continue  # A/B against an older build: entry points added since are absent
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

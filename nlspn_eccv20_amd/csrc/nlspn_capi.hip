@@ -415,8 +415,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (ng > kResMaxGroups) return false;
     const unsigned G = (unsigned)(S.Bg * S.gy * S.gx);
     if ((G + 1) * 4 > kSyncBytes) return false;
-    const size_t lds = 4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt;
-    if (lds > (size_t)kResLds || lds <= 80 * 1024) return false;  // > half a CU's LDS: one workgroup per CU
+    // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
+    // res_win_cells, may need less: the request is padded)
+    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt,
+                                        80 * 1024 + 16);
+    if (lds > (size_t)kResLds) return false;
     P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false) : res_fn<__half>(S.nt, false);
     P.block = (unsigned)S.nt;
     P.lds = lds;
@@ -771,16 +774,10 @@ static int launch_heads(HeadsArgs &a, void *stream) {
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 3>)};
         fn = abl[(a.dbg & 3u) - 1];
     }
-    if (lds > 65536) {  // once per kernel and size (idempotent, so an unlocked check is harmless)
-        static const void *set_fn[16];
-        static int set_lds[16];
-        int k = 0;
-        while (k < 16 && set_fn[k] && !(set_fn[k] == fn && set_lds[k] >= lds)) ++k;
-        if (k == 16 || !set_fn[k]) {
-            NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            if (k < 16) { set_lds[k] = lds; set_fn[k] = fn; }
-        }
-    }
+    // The attribute is per device: set it on every launch (the current device is the
+    // caller's, and DataParallel replicas launch from their own threads), as
+    // launch_resident does; a host-side call, no device work.
+    if (lds > 65536) NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kHdNT), args, (size_t)lds, as_stream(stream)));
     return check_launch("nlspn_head_epilogue");

@@ -115,6 +115,7 @@ __host__ __device__ constexpr int res_win_cells(int nt) {
                ? ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4)
                : 32764;
 }
+
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
 #ifndef NLSPN_RES_NOGP
 constexpr bool kResGeneralPath = true;
@@ -271,6 +272,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                                    (size_t)blockIdx.x * a.T * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
     const bool active = tid < nown;
+    const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
     if (active) {
         const int rr = tid / nqw;
@@ -362,7 +364,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1 - 1; ctl[3] = 4 * c0; ctl[4] = 4 * c1 - 1; }
     lds_barrier();
     if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
-    const float Hf = (float)H, Wf = (float)W;
     {
         int mn = r0, mx = r1 - 1, cmn = 4 * c0, cmx = 4 * c1 - 1;
 #pragma unroll
@@ -480,7 +481,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // columns left and right of it.  Iteration 1 stages the whole in-image window.
     const int ntop = r0 - ra, nband = (ntop + rb - r1 + 1) * wqn;
     const int side = wqn - nqw, left = c0 - qa;
-    const int nall = (rb - ra + 1) * wqn, nrest = nall - nown;
+    // wave-uniform: held in SGPRs (as VGPRs they were the loop's one scratch reload)
+    const int nall = __builtin_amdgcn_readfirstlane((rb - ra + 1) * wqn), nrest = __builtin_amdgcn_readfirstlane(nall - nown);
     const float rwqn = 1.0f / (float)wqn, rside = 1.0f / (float)(side > 0 ? side : 1);
 
     const T *p_all = static_cast<const T *>(a.pred_inter);
@@ -493,24 +495,21 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // publishes epoch + t + 1 after iteration t, so iteration t waits for epoch + t; the
     // first iteration of a launch waits for nothing (its source is an input).
     const int t0 = fused ? 0 : 1;
+    // The polling wave: the last one holding quads, not wave 0, whose lane 0 stores the
+    // progress word — a poll load queues behind that write-through store in its wave's
+    // vmcnt order, so polling from wave 0 added the store's round trip to every wait
+    // (same-box A/B: C2 134.0k vs 124.1k iters/s, trace wait 0.96 vs 1.56 us)
+    const int pwave = (nown - 1) >> 6;
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     for (int t = t0; t < a.T; ++t) {
-        // The tap geometry depends only on the (invariant) coordinates, so the
-        // compiler would hoist all 32 taps' weights and addresses out of this loop
-        // and spill them; opaque register moves keep them per iteration (no code).
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
-            asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
-        }
-        int tb = tid;  // likewise the staging indices (recomputed per iteration, not spilled)
-        asm volatile("" : "+v"(tb));
-
         unsigned long long *trace = ((a.dbg & 8u) && t > 0) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                                  ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
+        const bool first = t == 0;  // fused iteration 1: f = p0 * conf' from the raw inputs
+        const T *p_in = first ? static_cast<const T *>(a.pinit) + b * HW : p_all + (size_t)(t - 1) * a.tstride + b * HW;
+        const rsrc_t rp = make_rsrc(p_in);
         // ---- wait until every part this one reads has finished iteration t-1
-        if (t > t0 && tid < 64 && !(a.dbg & 1u)) {
+        if (t > t0 && (tid >> 6) == pwave && !(a.dbg & 1u)) {
             unsigned spins = 0;
             bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
             const unsigned need = epoch + (unsigned)t;
@@ -564,12 +563,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 
         // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
         // (written by other parts in this launch), conf' by plain loads (invariant)
-        const bool first = t == 0;  // fused iteration 1: f = p0 * conf' from the raw inputs
-        const T *p_in = first ? static_cast<const T *>(a.pinit) + b * HW : p_all + (size_t)(t - 1) * a.tstride + b * HW;
-        const rsrc_t rp = make_rsrc(p_in);
         // after a launch's first iteration the own quads are in the window already
         // (written back below), so only the other parts' quads are loaded
         const bool rim = t > t0;
+        // the staging index (= tid) rebuilt per iteration from the wave's base (an SGPR) and
+        // the lane id, so no VGPR holds it across the loop (it was spilled and reloaded)
+        const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int nsq_it = (a.dbg & 2u) ? 0 : (rim ? nrest : nall);
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
@@ -637,6 +636,15 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
+        // The tap geometry depends only on the (invariant) coordinates, so the
+        // compiler would hoist all 32 taps' weights and addresses out of the loop
+        // and spill them; opaque register moves keep them per iteration (no code).
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
+            asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
+        }
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
         if (active && !(a.dbg & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -656,8 +664,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     const float hh = 1.f - lh, hw = 1.f - lw;
                     const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
                     const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
-                    const float2 *sp = reinterpret_cast<const float2 *>(fwin + idx);
-                    const float2 s01 = sp[0], s23 = *reinterpret_cast<const float2 *>(fwin + idx + WW);
+                    const float2 s01 = *reinterpret_cast<const float2 *>(fwin + idx),
+                                 s23 = *reinterpret_cast<const float2 *>(fwin + idx + WW);
                     const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                     acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
                 }
@@ -668,9 +676,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // shares no registers with the branch-free path (no spills around it).
             if (kResGeneralPath && wave_fb && has_fb) {
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
-                int tq = tid;  // the own quad's row and first column, recomputed (not live across the loop)
-                asm volatile("" : "+v"(tq));
-                const int gr = tq / nqw, y = r0 + gr, x0 = 4 * (c0 + tq - gr * nqw);
+                // the own quad's row and first column, recomputed from its byte offset (not
+                // live across the loop)
+                const int pe = (int)(vpix / ES), y = pe / W, x0 = pe - y * W;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float s = 0.f;

@@ -37,6 +37,8 @@
 
 #include "nlspn_common.h"
 
+#include <type_traits>
+
 namespace nlspn {
 
 struct StepArgs {
@@ -252,9 +254,11 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
 
     // ---- 4. taps.  Pass A (LDS only, no divergent global loads, so the
     // compiler's vmcnt waits stay counted per tap): col[k] = bilinear * a_k for
-    // every tap whose 2x2 footprint is inside the window; out-of-window taps are
-    // flagged in `fb`.  Pass B (rare): flagged taps from L2/global with the
-    // reference's per-corner checks (their offsets re-read from cache).  Then
+    // every tap whose 2x2 footprint is inside the window (one range test; invalid taps
+    // there sample zeros, see lo_h below); taps outside it are flagged in `fb`.  Pass B
+    // (rare): flagged taps test validity (invalid: col = 0 * a stands) and the valid
+    // ones are sampled from L2/global with the reference's per-corner checks (their
+    // offsets re-read from cache).  Then
     // accumulate in tap index order with the reference tap (K/2) weighted
     // 1 - sum(others) (nlspnmodel.py:262-263): the reference's summation order,
     // whichever pass served a tap.  col = val * a then acc += col is the same
@@ -264,63 +268,82 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     for (int p = 0; p < PX; ++p) asum[p] = 0.f;
     const float Hf = (float)H, Wf = (float)W;
     const float yb_f = (float)(y - PH), xb_f = (float)(xb - PW);  // |values| < 2^24: exact
+    // One range test per tap: the footprint rows floor(h), floor(h)+1 lie in the window iff
+    // wy0 <= h < wy0 + WH - 1 (likewise w).  The window holds zeros outside the image, so
+    // an INVALID tap (outside (-1, H) x (-1, W), .cuh:180) whose footprint is in the
+    // window samples exactly +0 there — the reference's val = 0 — except at h == -1 or
+    // w == -1 exactly, where the in-image row / column enters with weight 0 (0 * f, NaN
+    // for a non-finite f): tiles whose window reaches above or left of the image zero
+    // those taps explicitly (a tile-uniform branch).  A tap outside the window (or NaN)
+    // goes to pass B, which tests validity first.
+    const float lo_h = (float)wy0, hi_h = (float)(wy0 + WH - 1);
+    const float lo_w = (float)wx0, hi_w = (float)(wx0 + WW - 1);
+    const bool edge_tile = wy0 < 0 || wx0 < 0;
+    // window byte offset of the footprint's top-left cell, from the floors in exact float
+    // arithmetic (small integers): 4 (floor(h) - wy0) WW + 4 (floor(w) - wx0)
+    const float wofs = -4.f * (float)(wy0 * WW + wx0);
     constexpr int NFB = (K * PX + 31) / 32;
     uint32_t fb[NFB];
 #pragma unroll
     for (int q = 0; q < NFB; ++q) fb[q] = 0u;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int t = k < REF ? k : k + 1;
-        const int i = t / KW, j = t % KW;
-        float ak[PX], tdh[PX], tdw[PX];
-        if (PRE) {
-#pragma unroll
-            for (int p = 0; p < PX; ++p) {
-                ak[p] = av[PRE ? k : 0][p];
-                tdh[p] = dh[PRE ? k : 0][p];
-                tdw[p] = dw[PRE ? k : 0][p];
-            }
-        } else {
-            BVec<T, PX>::load(ra, vpix, (unsigned)t * plane_bytes, ak);
-            if (OFFSET) {
-                const unsigned c = a.off_raw ? k : t;
-                BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, tdh);
-                BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, tdw);
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < PX; ++p) {
-            asum[p] += ak[p];
-            if (!OFFSET) {
-                col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
-                continue;
-            }
-            // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
-            // the tap's base coordinates as exact float sums of small integers (one add per
-            // tap instead of an integer add and a convert): the same values as
-            // (float)(y - PH + i) and (float)(xb + p - PW + j)
-            const float h_im = (yb_f + (float)i) + tdh[p];
-            const float w_im = (xb_f + (float)(p + j)) + tdw[p];
-            float v = 0.f;
-            if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                // inside (-1, H) x (-1, W): floor fits an int, and (float)h_low == fh, so
-                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36)
-                const float fh = floorf(h_im), fw = floorf(w_im);
-                const int h_low = (int)fh, w_low = (int)fw;
-                const int ry = h_low - wy0, rx = w_low - wx0;
-                if ((unsigned)ry < (unsigned)(WH - 1) && (unsigned)rx < (unsigned)(WW - 1)) {
-                    const float lh = h_im - fh, lw = w_im - fw;
-                    const float hh = 1.f - lh, hw = 1.f - lw;
-                    const float *s = &win[ry * WW + rx];
-                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
-                } else {
-                    fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);
+    // pass A, instantiated for edge tiles (the h == -1 / w == -1 fix-up) and the rest, so
+    // the tile-uniform choice is one branch outside the tap loop
+    auto pass_a = [&](auto edge) {
+        constexpr bool EDGE = decltype(edge)::value;
+    #pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = k < REF ? k : k + 1;
+            const int i = t / KW, j = t % KW;
+            float ak[PX], tdh[PX], tdw[PX];
+            if (PRE) {
+    #pragma unroll
+                for (int p = 0; p < PX; ++p) {
+                    ak[p] = av[PRE ? k : 0][p];
+                    tdh[p] = dh[PRE ? k : 0][p];
+                    tdw[p] = dw[PRE ? k : 0][p];
+                }
+            } else {
+                BVec<T, PX>::load(ra, vpix, (unsigned)t * plane_bytes, ak);
+                if (OFFSET) {
+                    const unsigned c = a.off_raw ? k : t;
+                    BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, tdh);
+                    BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, tdw);
                 }
             }
-            col[k][p] = v * ak[p];  // .cuh:189 col = val * mask
+    #pragma unroll
+            for (int p = 0; p < PX; ++p) {
+                asum[p] += ak[p];
+                if (!OFFSET) {
+                    col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
+                    continue;
+                }
+                // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
+                // the tap's base coordinates as exact float sums of small integers (one add per
+                // tap instead of an integer add and a convert): the same values as
+                // (float)(y - PH + i) and (float)(xb + p - PW + j)
+                const float h_im = (i == 0 ? yb_f : yb_f + (float)i) + tdh[p];  // yb_f + 0 == yb_f: never -0
+                const float w_im = (xb_f + (float)(p + j)) + tdw[p];
+                float v = 0.f;
+                if (h_im >= lo_h && h_im < hi_h && w_im >= lo_w && w_im < hi_w) {
+                    // valid and in the window: (float)h_low == fh, so h_im - fh is the
+                    // reference's h_im - (float)h_low (.cuh:35-36)
+                    const float fh = floorf(h_im), fw = floorf(w_im);
+                    const float lh = h_im - fh, lw = w_im - fw;
+                    const float hh = 1.f - lh, hw = 1.f - lw;
+                    const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
+                    const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
+                    if (EDGE && (h_im == -1.f || w_im == -1.f)) v = 0.f;  // invalid: val = 0
+                } else {
+                    fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);  // pass B
+                }
+                col[k][p] = v * ak[p];  // .cuh:189 col = val * mask
+            }
         }
-    }
+    };
+    if (edge_tile) pass_a(std::true_type{});
+    else pass_a(std::false_type{});
     uint32_t any_fb = 0u;
 #pragma unroll
     for (int q = 0; q < NFB; ++q) any_fb |= fb[q];
@@ -338,6 +361,8 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
                 const float h_im = (float)(y - PH + i) + o1[0];
                 BVec<T, 1>::load(ro, vpix + p * ES, (2 * c + 1) * plane_bytes, o1);
                 const float w_im = (float)(xb + p - PW + j) + o1[0];
+                // invalid (.cuh:180, NaN included): the reference's val = 0, already col = 0 * a above
+                if (!(h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf)) continue;
                 if (FIRST) a1[0] = av[PRE ? k : 0][p];  // normalised in registers above
                 else BVec<T, 1>::load(ra, vpix + p * ES, (unsigned)t * plane_bytes, a1);
                 const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);

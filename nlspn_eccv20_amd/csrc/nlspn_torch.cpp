@@ -50,6 +50,17 @@ void check_cuda(const char *name, const Tensor &t) { TORCH_CHECK(t.is_cuda(), na
 void check_cuda(const char *name, const optional<Tensor> &t) {
     if (t.has_value()) check_cuda(name, *t);
 }
+// An operand of an op whose kernels index every operand as `ref`'s element type on
+// `ref`'s device (the reference's data<scalar_t>() raises on a mismatch).
+void check_like(const char *name, const Tensor &t, const Tensor &ref) {
+    check_cuda(name, t);
+    TORCH_CHECK(t.device() == ref.device(), name, " is on ", t.device(), ", expected ", ref.device());
+    TORCH_CHECK(t.scalar_type() == ref.scalar_type(), name, " has dtype ", t.scalar_type(), ", expected ",
+                ref.scalar_type());
+}
+void check_like(const char *name, const optional<Tensor> &t, const Tensor &ref) {
+    if (t.has_value()) check_like(name, *t, ref);
+}
 const void *ptr(const optional<Tensor> &t) { return t.has_value() ? t->data_ptr() : nullptr; }
 void *mut_ptr(optional<Tensor> &t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
@@ -97,8 +108,10 @@ Tensor prop_step(const Tensor &feat, const optional<Tensor> &confidence, const o
     check_cuda("feat", feat);
     check_cuda("confidence", confidence);
     check_cuda("dep", dep);
-    check_cuda("aff", aff);
-    check_cuda("offset", offset);
+    check_like("aff", aff, feat);
+    check_like("offset", offset, feat);
+    check_like("confidence", confidence, feat);
+    check_like("dep", dep, feat);
     TORCH_CHECK(kh % 2 == 1 && kw % 2 == 1, "only odd kernel is supported but k_f = ", kh, "x", kw);
     const int64_t K = kh * kw - 1;
     TORCH_CHECK(feat.dim() == 4, "feat must be (B, 1, H, W)");
@@ -152,9 +165,12 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>, optional<Tensor>> propagate
     TORCH_CHECK(!preserve_input || dep.has_value(), "preserve_input requires dep");
     const int64_t abs = planes("aff", aff, B, K, H, W);
     const int64_t obs = offset.has_value() ? planes("offset", *offset, B, 2 * K, H, W) : 0;
-    TORCH_CHECK(aff.scalar_type() == pred_init.scalar_type() &&
-                    (!offset.has_value() || offset->scalar_type() == pred_init.scalar_type()),
-                "aff/offset must have pred_init's dtype");
+    check_like("aff", aff, pred_init);
+    check_like("offset", offset, pred_init);
+    check_like("dep", dep, pred_init);
+    check_like("confidence", confidence, pred_init);
+    TORCH_CHECK(gamma.device() == pred_init.device(), "gamma is on ", gamma.device(), ", expected ",
+                pred_init.device());
     const int dt = prop_dtype(pred_init);
     const Tensor g = gamma_f32(gamma);
     const auto o = pred_init.options();
@@ -194,10 +210,11 @@ Tensor mdcn_forward(const Tensor &input, const Tensor &weight, const optional<Te
     TORCH_CHECK(input.is_contiguous(), "input tensor has to be contiguous");
     TORCH_CHECK(weight.is_contiguous(), "weight tensor has to be contiguous");
     check_cuda("input", input);
-    check_cuda("weight", weight);
-    check_cuda("bias", bias);
-    check_cuda("offset", offset);
-    check_cuda("mask", mask);
+    check_like("weight", weight, input);
+    check_like("bias", bias, input);
+    check_like("offset", offset, input);
+    check_like("mask", mask, input);
+    TORCH_CHECK(input.dim() == 4 && weight.dim() == 4, "input and weight must be 4-D");
     const int64_t B = input.size(0), C = input.size(1), H = input.size(2), W = input.size(3);
     const int64_t Cout = weight.size(0);
     TORCH_CHECK(weight.size(2) == kernel_h && weight.size(3) == kernel_w, "Input shape and kernel shape wont match: (",
@@ -235,15 +252,27 @@ std::vector<Tensor> mdcn_backward(const Tensor &input, const Tensor &weight, con
     TORCH_CHECK(input.is_contiguous(), "input tensor has to be contiguous");
     TORCH_CHECK(weight.is_contiguous(), "weight tensor has to be contiguous");
     check_cuda("input", input);
-    check_cuda("grad_output", grad_output);
+    check_like("weight", weight, input);
+    check_like("bias", bias, input);
+    check_like("offset", offset, input);
+    check_like("mask", mask, input);
+    check_like("grad_output", grad_output, input);
+    TORCH_CHECK(input.dim() == 4 && weight.dim() == 4, "input and weight must be 4-D");
     const int64_t B = input.size(0), C = input.size(1), H = input.size(2), W = input.size(3);
     const int64_t Cout = weight.size(0);
+    const int64_t KK = kernel_h * kernel_w;
+    TORCH_CHECK(weight.size(2) == kernel_h && weight.size(3) == kernel_w && C == weight.size(1) * group,
+                "weight has shape ", weight.sizes());
+    TORCH_CHECK(bias.numel() == Cout, "bias has ", bias.numel(), " elements, expected ", Cout);
     TORCH_CHECK(C % group == 0 && Cout % group == 0, "channels(", C, ") and channels_out(", Cout,
                 ") must divide group(", group, ")");
     const int64_t Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) / stride_h + 1;
     const int64_t Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) / stride_w + 1;
     TORCH_CHECK(grad_output.sizes() == at::IntArrayRef({B, Cout, Ho, Wo}), "grad_out has shape ",
                 grad_output.sizes());
+    TORCH_CHECK(offset.sizes() == at::IntArrayRef({B, 2 * deformable_group * KK, Ho, Wo}), "offset has shape ",
+                offset.sizes());
+    TORCH_CHECK(mask.sizes() == at::IntArrayRef({B, deformable_group * KK, Ho, Wo}), "mask has shape ", mask.sizes());
     const Tensor off_c = offset.contiguous(), mask_c = mask.contiguous(), go = grad_output.contiguous();
     Tensor gi = at::empty_like(input), goff = at::empty_like(off_c), gm = at::empty_like(mask_c),
            gw = at::empty_like(weight);

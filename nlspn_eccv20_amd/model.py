@@ -297,6 +297,13 @@ class NLSPNModel(nn.Module):
         crop = lambda fd: None if fd is None else self._crop(fd, fe1)  # noqa: E731
         return fe1, crop(id_fd1), crop(off_aff_fd1), crop(cf_fd1)
 
+    def _head_cache(self):
+        """The packed head-weight cache, or None (pack per call) in a DataParallel replica:
+        replicas share this module's __dict__ (so the cache) while their parameters are
+        fresh broadcast copies whose storage and version counter can repeat across forwards
+        with different master weights (src/main.py:366 runs the model under DataParallel)."""
+        return None if getattr(self, "_is_replica", False) else self._head_weights
+
     def _fused_inference(self, fe1) -> bool:
         return fe1.is_cuda and not torch.is_grad_enabled() and fe1.dtype == torch.float32
 
@@ -307,7 +314,7 @@ class NLSPNModel(nn.Module):
             # inference: the three last convolutions + bias/activation as one HIP kernel
             # reading fe1 and the decoder outputs in place (heads.py, nlspn_heads.h)
             return head_epilogue(fe1, off_aff_fd1, self.off_aff_dec0, id_fd1, self.id_dec0, cf_fd1,
-                                 self.cf_dec0 if self.args.conf_prop else None, weights=self._head_weights)
+                                 self.cf_dec0 if self.args.conf_prop else None, weights=self._head_cache())
         pred_init = self.id_dec0(torch.cat((id_fd1, fe1), 1))
         off_aff = self.off_aff_dec0(torch.cat((off_aff_fd1, fe1), 1))
         confidence = None
@@ -346,10 +353,11 @@ class NLSPNModel(nn.Module):
         (propagation.propagate_normalized, :340-381).  The same output dict as
         propagate_heads, bit for bit given the same convolution sums."""
         a = self.args
+        dep = dep.contiguous().float()  # as head_epilogue_prologue coerces it; propagate_normalized takes the same
         h = head_epilogue_prologue(fe1, off_aff_fd1, self.off_aff_dec0, id_fd1, self.id_dec0, dep,
                                    self.aff_scale_const, a.affinity, cf_fd1,
                                    self.cf_dec0 if a.conf_prop else None, a.preserve_input, a.always_clip,
-                                   weights=self._head_weights)
+                                   weights=self._head_cache())
         o = propagate_normalized(h["p0"], dep if a.preserve_input else None, h["confidence"], h["aff"],
                                  h["offset"], a.prop_time, (3, 3), a.preserve_input, a.always_clip)
         return {"pred": o["pred"], "pred_init": h["pred_init"], "pred_inter": o["pred_inter"],

@@ -15,15 +15,28 @@ registered below give ``torch.compile`` the output shapes without running anythi
         -> (pred, pred_inter (T,B,1,H,W), aff, offset or None, confidence or None)   :323-381
   torch.ops.nlspn.modulated_deform_conv_forward / _backward        vision.cpp:9-10
 
-The ops are inference building blocks (no autograd formula registered); the
-differentiable forms stay ``nlspn_eccv20_amd.propagate`` / ``prop_step`` /
-``dcn.ModulatedDeformConvFunction``.
+Autograd (round 3): every forward op has a backward registered
+(torch.library.register_autograd), built on the same HIP backward entry points as the
+ctypes autograd functions of propagation.py / dcn.py — the reference's DCN is
+differentiable wherever ModulatedDeformConvFunction appears
+(modulated_deform_conv_func.py:38-56).  The backward passes are ops too, so
+torch.compile traces a training step through them:
+
+  torch.ops.nlspn.propagate_backward             nlspn_propagate_backward (the section)
+  torch.ops.nlspn.prop_step_backward             nlspn_prop_step_backward (raw offsets, float32)
+  torch.ops.nlspn.affinity_normalization_backward  nlspn_affinity_normalize_backward
+  torch.ops.nlspn.modulated_deform_conv_backward  (the seam-2 op above)
+
+Gradients flow from pred / pred_inter of ``propagate`` (its aff / offset / confidence
+outputs are the output dict's copies and take no gradient, as in propagation.propagate).
 """
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import torch
+from torch import Tensor
 
 from . import _lib
 
@@ -45,6 +58,7 @@ def load() -> None:
         raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
     torch.ops.load_library(LIB_PATH)
     _register_fakes()
+    _register_autograd()
     _loaded = True
 
 
@@ -89,3 +103,117 @@ def _register_fakes() -> None:
                      ("propagate", fake_propagate), ("modulated_deform_conv_forward", fake_mdcn_fwd),
                      ("modulated_deform_conv_backward", fake_mdcn_bwd)):
         torch.library.register_fake(f"nlspn::{name}")(fn)
+
+
+def _register_autograd() -> None:
+    from . import propagation as P
+
+    def _z(t):
+        return t.new_empty((0,))
+
+    # ---- backward ops (custom ops over the ctypes backward paths; fake kernels for compile)
+    @torch.library.custom_op("nlspn::propagate_backward", mutates_args=())
+    def propagate_backward(pred_init: Tensor, dep: Optional[Tensor], confidence: Optional[Tensor], aff: Tensor,
+                           offset: Optional[Tensor], gamma: Tensor, pred_inter: Tensor, aff_norm: Tensor,
+                           conf_eff: Optional[Tensor], g_pred: Optional[Tensor], g_inter: Optional[Tensor], kh: int,
+                           kw: int, affinity: str, preserve_input: bool,
+                           always_clip: bool) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+        g_pi, g_conf, g_aff, g_off, g_gamma, _ = P._section_backward(
+            pred_init, dep, confidence, aff, offset, gamma, pred_inter, aff_norm, conf_eff, g_pred, g_inter, kh, kw,
+            pred_inter.shape[0], affinity, preserve_input, always_clip)
+        return (g_pi, _z(pred_init) if g_conf is None else g_conf, g_aff, _z(pred_init) if g_off is None else g_off,
+                torch.zeros_like(gamma) if g_gamma is None else g_gamma)
+
+    @propagate_backward.register_fake
+    def _(pred_init, dep, confidence, aff, offset, gamma, pred_inter, aff_norm, conf_eff, g_pred, g_inter, kh, kw,
+          affinity, preserve_input, always_clip):
+        B, _, H, W = pred_init.shape
+        K = kh * kw - 1
+        e = pred_init.new_empty
+        return (e((B, 1, H, W)), e((B, 1, H, W)) if confidence is not None else e((0,)), e((B, K, H, W)),
+                e((B, 2 * K, H, W)) if offset is not None else e((0,)), torch.empty_like(gamma))
+
+    @torch.library.custom_op("nlspn::prop_step_backward", mutates_args=())
+    def prop_step_backward(feat: Tensor, confidence: Optional[Tensor], dep: Optional[Tensor], aff: Tensor,
+                           offset: Optional[Tensor], g_out: Tensor, kh: int, kw: int, preserve_input: bool,
+                           always_clip: bool) -> tuple[Tensor, Tensor, Tensor, Tensor]:
+        g_feat, g_conf, g_aff, g_off = P._step_backward(feat, confidence, dep, aff, offset, g_out, kh, kw,
+                                                        preserve_input, always_clip)
+        return g_feat, _z(feat) if g_conf is None else g_conf, g_aff, _z(feat) if g_off is None else g_off
+
+    @prop_step_backward.register_fake
+    def _(feat, confidence, dep, aff, offset, g_out, kh, kw, preserve_input, always_clip):
+        B, _, H, W = feat.shape
+        K = kh * kw - 1
+        e = feat.new_empty
+        return (e((B, 1, H, W)), e((B, 1, H, W)) if confidence is not None else e((0,)), e((B, K + 1, H, W)),
+                e((B, 2 * K, H, W)) if offset is not None else e((0,)))
+
+    @torch.library.custom_op("nlspn::affinity_normalization_backward", mutates_args=())
+    def affinity_normalization_backward(aff: Tensor, gamma: Tensor, g_out: Tensor,
+                                        kind: str) -> tuple[Tensor, Tensor]:
+        g_raw, g_gamma = P._affnorm_backward(aff, gamma, g_out, kind)
+        return g_raw, torch.zeros_like(gamma) if g_gamma is None else g_gamma
+
+    @affinity_normalization_backward.register_fake
+    def _(aff, gamma, g_out, kind):
+        return torch.empty_like(aff, dtype=torch.float32), torch.empty_like(gamma)
+
+    # ---- autograd of the forward ops
+    def setup_propagate(ctx, inputs, output):
+        pred_init, dep, confidence, aff, offset, gamma, _T, kh, kw, affinity, preserve_input, always_clip = inputs
+        _pred, pred_inter, aff_out, _off, conf_out = output
+        ctx.save_for_backward(pred_init, dep, confidence, aff, offset, gamma, pred_inter, aff_out, conf_out)
+        ctx.cfg = (kh, kw, affinity, preserve_input, always_clip)
+
+    def bwd_propagate(ctx, g_pred, g_inter, _g_aff, _g_off, _g_conf):
+        pred_init, dep, confidence, aff, offset, gamma, pred_inter, aff_out, conf_out = ctx.saved_tensors
+        kh, kw, affinity, pre, clip = ctx.cfg
+        gp, gc, ga, go, gg = torch.ops.nlspn.propagate_backward(pred_init, dep, confidence, aff, offset, gamma,
+                                                                pred_inter, aff_out, conf_out, g_pred, g_inter, kh,
+                                                                kw, affinity, pre, clip)
+        return (gp, None, gc if confidence is not None else None, ga, go if offset is not None else None,
+                gg if affinity == "TGASS" else None) + (None,) * 6
+
+    torch.library.register_autograd("nlspn::propagate", bwd_propagate, setup_context=setup_propagate)
+
+    def setup_step(ctx, inputs, output):
+        feat, confidence, dep, aff, offset, kh, kw, raw_offsets, preserve_input, always_clip = inputs
+        if offset is not None and not raw_offsets:
+            raise NotImplementedError("nlspn::prop_step's backward takes raw_offsets=True (B, 2K, H, W) offsets")
+        ctx.save_for_backward(feat, confidence, dep, aff, offset)
+        ctx.cfg = (kh, kw, preserve_input, always_clip)
+
+    def bwd_step(ctx, g_out):
+        feat, confidence, dep, aff, offset = ctx.saved_tensors
+        gf, gc, ga, go = torch.ops.nlspn.prop_step_backward(feat, confidence, dep, aff, offset, g_out, *ctx.cfg)
+        return (gf, gc if confidence is not None else None, None, ga, go if offset is not None else None) + \
+            (None,) * 5
+
+    torch.library.register_autograd("nlspn::prop_step", bwd_step, setup_context=setup_step)
+
+    def setup_affnorm(ctx, inputs, output):
+        aff, gamma, kind = inputs
+        ctx.save_for_backward(aff, gamma)
+        ctx.kind = kind
+
+    def bwd_affnorm(ctx, g_out):
+        aff, gamma = ctx.saved_tensors
+        g_raw, g_gamma = torch.ops.nlspn.affinity_normalization_backward(aff, gamma, g_out, ctx.kind)
+        return g_raw, g_gamma if ctx.kind == "TGASS" else None, None
+
+    torch.library.register_autograd("nlspn::affinity_normalization", bwd_affnorm, setup_context=setup_affnorm)
+
+    def setup_mdcn(ctx, inputs, output):
+        inp, weight, bias, offset, mask = inputs[:5]
+        ctx.save_for_backward(inp, weight, bias, offset, mask)
+        ctx.ints = tuple(inputs[5:])
+
+    def bwd_mdcn(ctx, g_out):
+        inp, weight, bias, offset, mask = ctx.saved_tensors
+        b = bias if bias is not None else weight.new_zeros((weight.shape[0],))
+        gi, goff, gm, gw, gb = torch.ops.nlspn.modulated_deform_conv_backward(inp, weight, b, offset, mask,
+                                                                             g_out.contiguous(), *ctx.ints)
+        return (gi, gw, gb if bias is not None else None, goff, gm) + (None,) * 11
+
+    torch.library.register_autograd("nlspn::modulated_deform_conv_forward", bwd_mdcn, setup_context=setup_mdcn)

@@ -128,23 +128,30 @@ class _AffNormFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, g_out):
         aff, gamma = ctx.saved_tensors
-        if aff.dtype != torch.float32:
-            raise NotImplementedError("the affinity-normalisation backward is implemented for float32 storage")
-        B, K, H, W = aff.shape
-        f32 = dict(dtype=torch.float32, device=aff.device)
-        g_out = g_out.contiguous()
-        g_raw = torch.empty((B, K, H, W), **f32)
-        want_g = ctx.kind == "TGASS" and ctx.needs_input_grad[1]
-        g_gamma = torch.empty(1, **f32) if want_g else None
-        lib = _lib.get()
-        ws = torch.empty(max(1, lib.nlspn_affinity_normalize_backward_workspace_bytes(B, K, H, W) // 4), **f32)
-        with torch.cuda.device(aff.device):
-            _lib.check(lib.nlspn_affinity_normalize_backward(
-                _lib.DTYPE_F32, _ptr(aff), _planes("aff", aff, B, K, H, W), _ptr(_gamma_f32(gamma)), _ptr(g_out),
-                _ptr(g_raw), _ptr(g_gamma), _ptr(ws), B, K, H, W, _lib.AFF_KINDS[ctx.kind], _stream(aff.device)))
-        if g_gamma is not None:
-            g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype)
+        g_raw, g_gamma = _affnorm_backward(aff, gamma, g_out, ctx.kind, ctx.needs_input_grad[1])
         return g_raw, g_gamma, None
+
+
+def _affnorm_backward(aff, gamma, g_out, kind, want_gamma=True):
+    """nlspn_affinity_normalize_backward: gradients of the (K+1)-tap normalised affinity
+    with respect to the raw taps and (TGASS, want_gamma) gamma (else None)."""
+    if aff.dtype != torch.float32:
+        raise NotImplementedError("the affinity-normalisation backward is implemented for float32 storage")
+    B, K, H, W = aff.shape
+    f32 = dict(dtype=torch.float32, device=aff.device)
+    g_out = g_out.contiguous()
+    g_raw = torch.empty((B, K, H, W), **f32)
+    want_g = kind == "TGASS" and want_gamma
+    g_gamma = torch.empty(1, **f32) if want_g else None
+    lib = _lib.get()
+    ws = torch.empty(max(1, lib.nlspn_affinity_normalize_backward_workspace_bytes(B, K, H, W) // 4), **f32)
+    with torch.cuda.device(aff.device):
+        _lib.check(lib.nlspn_affinity_normalize_backward(
+            _lib.DTYPE_F32, _ptr(aff), _planes("aff", aff, B, K, H, W), _ptr(_gamma_f32(gamma)), _ptr(g_out),
+            _ptr(g_raw), _ptr(g_gamma), _ptr(ws), B, K, H, W, _lib.AFF_KINDS[kind], _stream(aff.device)))
+    if g_gamma is not None:
+        g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype)
+    return g_raw, g_gamma
 
 
 def affinity_normalization(aff: torch.Tensor, gamma: torch.Tensor, kind: str = "TGASS") -> torch.Tensor:
@@ -216,27 +223,35 @@ class _PropStepFn(torch.autograd.Function):
     def backward(ctx, g_out):
         feat, conf, dep, aff, off = ctx.saved_tensors
         (kh, kw), layout, preserve, clip = ctx.cfg
-        if feat.dtype != torch.float32:
-            raise NotImplementedError("the prop_step backward is implemented for float32 storage")
         if off is not None and layout != "raw":
             raise NotImplementedError("the prop_step backward takes offset_layout='raw' (B, 2K, H, W) offsets")
-        B, _, H, W = feat.shape
-        K = kh * kw - 1
-        f32 = dict(dtype=torch.float32, device=feat.device)
-        g_feat = torch.empty((B, 1, H, W), **f32)
-        g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
-        g_aff = torch.empty((B, K + 1, H, W), **f32)
-        g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
-        lib = _lib.get()
-        ws = torch.empty(lib.nlspn_prop_step_backward_workspace_bytes(B, H, W) // 4, **f32)
-        flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
-        with torch.cuda.device(feat.device):
-            _lib.check(lib.nlspn_prop_step_backward(
-                _lib.DTYPE_F32, _ptr(feat), _ptr(conf), _ptr(dep), _ptr(aff), _planes("aff", aff, B, K + 1, H, W),
-                _ptr(off), _planes("offset", off, B, 2 * K, H, W) if off is not None else 0,
-                _ptr(g_out.contiguous()), _ptr(g_feat), _ptr(g_conf), _ptr(g_aff), _ptr(g_off), _ptr(ws),
-                B, H, W, kh, kw, flags, _stream(feat.device)))
+        g_feat, g_conf, g_aff, g_off = _step_backward(feat, conf, dep, aff, off, g_out, kh, kw, preserve, clip)
         return g_feat, g_conf, None, g_aff, g_off, None, None, None, None
+
+
+def _step_backward(feat, conf, dep, aff, off, g_out, kh, kw, preserve, clip):
+    """nlspn_prop_step_backward: gradients of one iteration with respect to feat,
+    confidence, the normalised (K+1)-tap affinity (tap K/2 zero: recomputed in-kernel as
+    1 - sum) and the raw offsets (None where the input is absent)."""
+    if feat.dtype != torch.float32:
+        raise NotImplementedError("the prop_step backward is implemented for float32 storage")
+    B, _, H, W = feat.shape
+    K = kh * kw - 1
+    f32 = dict(dtype=torch.float32, device=feat.device)
+    g_feat = torch.empty((B, 1, H, W), **f32)
+    g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
+    g_aff = torch.empty((B, K + 1, H, W), **f32)
+    g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+    lib = _lib.get()
+    ws = torch.empty(lib.nlspn_prop_step_backward_workspace_bytes(B, H, W) // 4, **f32)
+    flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
+    with torch.cuda.device(feat.device):
+        _lib.check(lib.nlspn_prop_step_backward(
+            _lib.DTYPE_F32, _ptr(feat), _ptr(conf), _ptr(dep), _ptr(aff), _planes("aff", aff, B, K + 1, H, W),
+            _ptr(off), _planes("offset", off, B, 2 * K, H, W) if off is not None else 0,
+            _ptr(g_out.contiguous()), _ptr(g_feat), _ptr(g_conf), _ptr(g_aff), _ptr(g_off), _ptr(ws),
+            B, H, W, kh, kw, flags, _stream(feat.device)))
+    return g_feat, g_conf, g_aff, g_off
 
 
 def prop_step(feat: torch.Tensor, confidence: Optional[torch.Tensor], dep: Optional[torch.Tensor],
@@ -346,41 +361,53 @@ class _PropagateFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, g_pred, g_inter, _g_aff, _g_off, _g_conf):
         pred_init, dep, conf, aff, off, gamma, pred_inter, aff_norm, conf_eff = ctx.saved_tensors
-        kh, kw, T, affinity, preserve, clip = ctx.cfg
-        if pred_init.dtype != torch.float32:
-            raise NotImplementedError("the propagation backward is implemented for float32 storage")
-        B, _, H, W = pred_init.shape
-        K = kh * kw - 1
-        dev = pred_init.device
-        f32 = dict(dtype=torch.float32, device=dev)
-        g_pred = None if g_pred is None else g_pred.contiguous()
-        g_inter = None if g_inter is None else g_inter.contiguous()
-        g_pi = torch.empty((B, 1, H, W), **f32)
-        g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
-        if ctx.packed:  # one (B, 3K, H, W) gradient: offsets in planes 0..2K-1, affinity after
-            g_oa = torch.empty((B, 3 * K, H, W), **f32)
-            g_off, g_aff, gbs = g_oa[:, :2 * K], g_oa[:, 2 * K:], 3 * K * H * W
-        else:
-            g_aff = torch.empty((B, K, H, W), **f32)
-            g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
-            gbs = 0
-        g_gamma = torch.zeros(1, **f32)
-        lib = _lib.get()
-        ws = torch.empty(lib.nlspn_backward_workspace_bytes(B, H, W, kh, kw) // 4, **f32)
-        g = _gamma_f32(gamma)
-        flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
-        abs_ = _planes("aff", aff, B, K, H, W)
-        obs = _planes("offset", off, B, 2 * K, H, W) if off is not None else 0
-        with torch.cuda.device(dev):
-            _lib.check(lib.nlspn_propagate_backward(
-                _lib.DTYPE_F32, _ptr(pred_init), _ptr(dep), _ptr(conf), _ptr(aff), abs_, _ptr(off), obs, _ptr(g),
-                _ptr(pred_inter), _ptr(aff_norm), _ptr(conf_eff), _ptr(g_pred), _ptr(g_inter), _ptr(g_pi),
-                _ptr(g_conf), _ptr(g_aff), gbs, _ptr(g_off), gbs, _ptr(g_gamma), _ptr(ws), B, H, W, kh, kw, T,
-                _lib.AFF_KINDS[affinity], flags, _stream(dev)))
-        g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype) if affinity == "TGASS" else None
+        g_pi, g_conf, g_aff, g_off, g_gamma, g_oa = _section_backward(
+            pred_init, dep, conf, aff, off, gamma, pred_inter, aff_norm, conf_eff, g_pred, g_inter, *ctx.cfg,
+            packed=ctx.packed)
         if ctx.packed:
             return (g_pi, None, g_conf, None, None, g_gamma) + (None,) * 6 + (g_oa,)
         return (g_pi, None, g_conf, g_aff, g_off, g_gamma) + (None,) * 7
+
+
+def _section_backward(pred_init, dep, conf, aff, off, gamma, pred_inter, aff_norm, conf_eff, g_pred, g_inter,
+                      kh, kw, T, affinity, preserve, clip, packed=False):
+    """nlspn_propagate_backward: gradients of the section (pred, pred_inter) with respect
+    to pred_init, confidence, the raw affinity, the raw offsets and gamma (None where the
+    input is absent; g_gamma None unless TGASS).  packed: the affinity and offset
+    gradients as slices of one (B, 3K, H, W) buffer, returned last (else None)."""
+    if pred_init.dtype != torch.float32:
+        raise NotImplementedError("the propagation backward is implemented for float32 storage")
+    B, _, H, W = pred_init.shape
+    K = kh * kw - 1
+    dev = pred_init.device
+    f32 = dict(dtype=torch.float32, device=dev)
+    g_pred = None if g_pred is None else g_pred.contiguous()
+    g_inter = None if g_inter is None else g_inter.contiguous()
+    g_pi = torch.empty((B, 1, H, W), **f32)
+    g_conf = torch.empty((B, 1, H, W), **f32) if conf is not None else None
+    g_oa = None
+    if packed:  # one (B, 3K, H, W) gradient: offsets in planes 0..2K-1, affinity after
+        g_oa = torch.empty((B, 3 * K, H, W), **f32)
+        g_off, g_aff, gbs = g_oa[:, :2 * K], g_oa[:, 2 * K:], 3 * K * H * W
+    else:
+        g_aff = torch.empty((B, K, H, W), **f32)
+        g_off = torch.empty((B, 2 * K, H, W), **f32) if off is not None else None
+        gbs = 0
+    g_gamma = torch.zeros(1, **f32)
+    lib = _lib.get()
+    ws = torch.empty(lib.nlspn_backward_workspace_bytes(B, H, W, kh, kw) // 4, **f32)
+    g = _gamma_f32(gamma)
+    flags = (_lib.PRESERVE_INPUT if preserve else 0) | (_lib.ALWAYS_CLIP if clip else 0)
+    abs_ = _planes("aff", aff, B, K, H, W)
+    obs = _planes("offset", off, B, 2 * K, H, W) if off is not None else 0
+    with torch.cuda.device(dev):
+        _lib.check(lib.nlspn_propagate_backward(
+            _lib.DTYPE_F32, _ptr(pred_init), _ptr(dep), _ptr(conf), _ptr(aff), abs_, _ptr(off), obs, _ptr(g),
+            _ptr(pred_inter), _ptr(aff_norm), _ptr(conf_eff), _ptr(g_pred), _ptr(g_inter), _ptr(g_pi),
+            _ptr(g_conf), _ptr(g_aff), gbs, _ptr(g_off), gbs, _ptr(g_gamma), _ptr(ws), B, H, W, kh, kw, T,
+            _lib.AFF_KINDS[affinity], flags, _stream(dev)))
+    g_gamma = g_gamma.reshape(gamma.shape).to(gamma.dtype) if affinity == "TGASS" else None
+    return g_pi, g_conf, g_aff, g_off, g_gamma, g_oa
 
 
 def _packed_head(aff, offset):

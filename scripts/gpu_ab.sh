@@ -11,7 +11,7 @@ for r in 1 2 3; do
     [ "$rest" != "$lib" ] && envs=${rest#*:}
     ( if [ "$lib" != "-" ]; then export NLSPN_LIB_PATH=$lib; else unset NLSPN_LIB_PATH; fi
       for e in ${envs//,/ }; do export "$e"; done
-      timeout -k 10 120 python bench.py --config $CFG --no-cpu-baseline --no-backward --no-gru --no-extra-configs \
+      timeout -k 10 120 python bench.py --config $CFG --no-cpu-baseline --no-backward --no-gru --no-extra-configs --no-heads \
           --steps 200 --warmup 20 > $O/$name$r.json 2> $O/$name$r.err ) || exit 1
     python -c "import json;d=json.load(open('$O/$name$r.json'));print('$name', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_mean'])"
   done

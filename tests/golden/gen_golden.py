@@ -28,7 +28,15 @@ substituted on the generated paths):
   * s2d_*:  S2D.forward (:406-462) on seeded sparse depth, with its pool_convs and
     conv weights and the pool pyramid (captured by a forward hook on pool_convs).
 
-Outputs: tests/golden/*.npz (float32, allow_pickle=False) + manifest.json.
+Round 3 adds the offset branch (verdict r2 item 3):
+  * offloop_*:  NLSPNModel.forward with offset=True, T=18, prop_kernel 3 and 5, offsets
+    N(0,2^2) and N(0,50^2), always_clip on and off.  The `DCN` stub gets a
+    modulated_deform_conv_forward (grid_sample_dcn below) written from the DCNv2
+    definition on torch.grid_sample — independent of oracle/ — so the reference's own
+    offset-branch plumbing (_off_insert -> DCN offset channels, aff as the mask,
+    padding, loop, blends) runs end to end.
+
+Outputs: tests/golden/*.npz (float32 / float16-exact inputs, allow_pickle=False) + manifest.json.
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [--cases gru,s2d]
 """
 from __future__ import annotations
@@ -157,6 +165,90 @@ def gen_gru(nl, save, seed):
         save(name, f"forward with use_GRU=True (ConvGRU hidden/input {hd}), no offset, T={T}, {kw}", **arrs)
 
 
+def grid_sample_dcn(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
+                    dilation_h, dilation_w, group, deformable_group, im2col_step):
+    """A stand-in for DCN.modulated_deform_conv_forward (the signature of vision.cpp:9),
+    written from the DCNv2 definition, NOT from this repo's oracle: every tap t = i*kw + j
+    samples the input at (y*sh - ph + i*dh + offset[2t], x*sw - pw + j*dw + offset[2t+1])
+    bilinearly with zeros outside the image — torch.nn.functional.grid_sample(padding_mode=
+    "zeros", align_corners=True), which is 0 for points outside (-1, H) x (-1, W) as the
+    reference's validity test (.cuh:180) makes it — times mask[t]; then the convolution
+    sum over (channel, tap) with `weight`, plus `bias`.  Computed in float64 and returned
+    in the input's dtype, so it rounds once where the reference's float32 CUDA kernel
+    rounds per operation (~1e-7 relative)."""
+    import torch.nn.functional as F
+    assert group == 1 and deformable_group == 1, "the NLSPN call: one group, one deformable group"
+    x = input.double()
+    B, C, H, W = x.shape
+    Cout = weight.shape[0]
+    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    ys = (torch.arange(Ho, dtype=torch.float64) * stride_h - pad_h).view(1, Ho, 1)
+    xs = (torch.arange(Wo, dtype=torch.float64) * stride_w - pad_w).view(1, 1, Wo)
+    off, msk = offset.double(), mask.double()
+    out = torch.zeros(B, Cout, Ho, Wo, dtype=torch.float64)
+    for i in range(kernel_h):
+        for j in range(kernel_w):
+            t = i * kernel_w + j
+            h = ys + i * dilation_h + off[:, 2 * t]
+            w = xs + j * dilation_w + off[:, 2 * t + 1]
+            grid = torch.stack((2.0 * w / (W - 1) - 1.0, 2.0 * h / (H - 1) - 1.0), dim=-1)
+            val = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+            col = val * msk[:, t:t + 1]
+            out += torch.einsum("oc,bchw->bohw", weight[:, :, i, j].double(), col)
+    if bias is not None:
+        out += bias.double().view(1, Cout, 1, 1)
+    return out.to(input.dtype)
+
+
+OFFSET_CASES = [  # (name, prop_kernel, offset sigma, shape (B, H, W), flags): nlspnmodel.py:204-208 via the DCN stand-in
+    ("offloop_k3_s2_tgass", 3, 2.0, (2, 40, 56), dict(affinity="TGASS", preserve_input=True, always_clip=False,
+                                                      conf_prop=True)),
+    ("offloop_k3_s2_ass_clip_noconf", 3, 2.0, (1, 40, 56), dict(affinity="ASS", preserve_input=True,
+                                                               always_clip=True, conf_prop=False)),
+    ("offloop_k3_s50_tgass_clip", 3, 50.0, (1, 40, 56), dict(affinity="TGASS", preserve_input=True, always_clip=True,
+                                                             conf_prop=True)),
+    ("offloop_k5_s2_tgass", 5, 2.0, (1, 32, 40), dict(affinity="TGASS", preserve_input=True, always_clip=False,
+                                                      conf_prop=True)),
+    ("offloop_k5_s50_tc_nopreserve", 5, 50.0, (1, 32, 40), dict(affinity="TC", preserve_input=False,
+                                                               always_clip=False, conf_prop=True)),
+]
+OFFLOOP_KEEP = (0, 8, 17)  # pred_inter planes kept in the fixtures (size)
+
+
+def gen_offset(nl, save, seed):
+    """The reference's offset branch end to end: NLSPNModel.forward with offset=True,
+    whose _propagate_once calls ModulatedDeformConvFunction.apply (nlspnmodel.py:204-208
+    -> modulated_deform_conv_func.py:26-34 -> DCN.modulated_deform_conv_forward), with
+    the CUDA extension replaced by grid_sample_dcn.  What the fixtures pin is the
+    reference-side plumbing of that branch: _off_insert's channel layout feeding the
+    DCN's 2t / 2t+1 offset channels, the normalised affinity as the mask, self.padding,
+    the weight/bias, the loop and blends.  Inputs are stored as float16-exact values
+    (fixture size); the reference computes on them in float32."""
+    dcn = sys.modules["DCN"]
+    dcn.modulated_deform_conv_forward = grid_sample_dcn
+    g = torch.Generator().manual_seed(seed)
+    for name, pk, sigma, (B, H, W), kw in OFFSET_CASES:
+        m = make_model(nl, prop_kernel=pk, prop_time=18, offset=True, **kw)
+        K = m.num_neighbors
+        pred_init, dep, conf, _ = synth(g, B, H, W, K, density=0.05)
+        aff = torch.randn(B, K, H, W, generator=g).abs()
+        off = torch.randn(B, 2 * K, H, W, generator=g) * sigma
+        q = lambda t: t.half().float()  # noqa: E731
+        pred_init, conf, aff, off = q(pred_init), q(conf), q(aff), q(off)
+        dep = q(dep)
+        off_aff = torch.cat([off, aff], 1)
+        o = run_forward(m, pred_init, dep, off_aff, conf if kw["conf_prop"] else None)
+        inter = torch.stack(o["pred_inter"], 0)
+        arrs = dict(pred_init=pred_init.half(), dep=dep.half(), off_aff=off_aff.half(),
+                    gamma=m.aff_scale_const.detach().reshape(1), pred=o["pred"],
+                    pred_inter_sel=inter[list(OFFLOOP_KEEP)], offset=o["offset"].half())
+        if kw["conf_prop"]:
+            arrs.update(conf=conf.half(), confidence=o["confidence"])
+        save(name, f"forward offset=True (DCN = grid_sample stand-in), prop_kernel={pk}, offsets N(0,{sigma}^2), "
+             f"B,H,W={B},{H},{W}, T=18, pred_inter planes {list(OFFLOOP_KEEP)}, {kw}", **arrs)
+
+
 def gen_s2d(nl, save, seed):
     for n, (B, H, W, density) in enumerate(((2, 20, 28, 0.08), (1, 13, 17, 0.5))):
         torch.manual_seed(seed + n)
@@ -177,9 +269,9 @@ def gen_s2d(nl, save, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT_DIR)
-    ap.add_argument("--cases", default="all", help="comma list of: base, gru, s2d (default all)")
+    ap.add_argument("--cases", default="all", help="comma list of: base, gru, s2d, offset (default all)")
     a = ap.parse_args()
-    which = {"base", "gru", "s2d"} if a.cases == "all" else set(a.cases.split(","))
+    which = {"base", "gru", "s2d", "offset"} if a.cases == "all" else set(a.cases.split(","))
     nl = import_reference()
     torch.set_num_threads(1)
     mpath = os.path.join(a.out, "manifest.json")
@@ -200,6 +292,8 @@ def main():
         gen_gru(nl, save, SEED + 1000)
     if "s2d" in which:
         gen_s2d(nl, save, SEED + 2000)
+    if "offset" in which:
+        gen_offset(nl, save, SEED + 3000)
     if "base" not in which:
         with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)

@@ -68,7 +68,7 @@ def test_fused_prologue_bitexact(kind, preserve, clip):
 
 @pytest.mark.parametrize("B,C,H,W,T,with_cf", [
     (2, 64, 228, 304, 18, True),   # NYU size: the resident path
-    (3, 32, 37, 52, 6, True),      # W % 4 != 0: per-iteration steps, partial tiles
+    (3, 32, 37, 50, 6, True),      # W % 4 != 0: scalar kernels, per-iteration steps, partial tiles
     (1, 16, 24, 32, 1, False),     # T = 1, no confidence head
     (2, 16, 24, 32, 2, True),      # T = 2
 ])
@@ -76,6 +76,15 @@ def test_fused_prologue_shapes(B, C, H, W, T, with_cf):
     oa, idc, cfc, src, dep = _case(B, C, H, W, seed=2, with_cf=with_cf)
     gamma = torch.tensor([4.0], device=DEV)
     _assert_same(*_run_both(oa, idc, cfc, src, dep, gamma, "TGASS", T, True, False), with_cf)
+
+
+def test_fused_prologue_per_iteration_path(monkeypatch):
+    """propagate_normalized's per-iteration fallback (NLSPN_RESIDENT=0) at a width the
+    resident kernel would take: the same bits as the unfused path."""
+    monkeypatch.setenv("NLSPN_RESIDENT", "0")
+    oa, idc, cfc, src, dep = _case(2, 16, 40, 64, seed=4)
+    gamma = torch.tensor([4.0], device=DEV)
+    _assert_same(*_run_both(oa, idc, cfc, src, dep, gamma, "TGASS", 7, True, False), True)
 
 
 def test_fused_prologue_negative_depth_clip():
@@ -116,3 +125,47 @@ def test_model_forward_fused_equals_unfused():
     assert all(torch.equal(a, b) for a, b in zip(fused["pred_inter"], ref["pred_inter"]))
     for k in ("pred", "aff", "offset"):  # up to the decoder's run-to-run rounding
         assert torch.allclose(whole[k], ref[k], rtol=1e-4, atol=1e-4), k
+
+
+def test_model_forward_fused_coerces_dep():
+    """The fused inference path accepts the depth batches the unfused path does (ADVICE
+    r2): a non-contiguous or float64 dep gives the float32-contiguous result."""
+    import types
+    from nlspn_eccv20_amd import NLSPNModel
+    args = types.SimpleNamespace(prop_kernel=3, affinity="TGASS", affinity_gamma=0.5, prop_time=6,
+                                 preserve_input=True, always_clip=False, conf_prop=True, offset=True,
+                                 network="resnet18", from_scratch=True, zero_init_aff=False, use_GRU=False,
+                                 use_S2D=False, GRU_hidden_dim=8, GRU_input_dim=8, lr=1e-3, max_depth=10.0,
+                                 patch_height=48, patch_width=80, model_name="NLSPN")
+    torch.manual_seed(0)
+    m = NLSPNModel(args).to(DEV).eval()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    rgb = torch.rand((2, 3, 48, 80), device=DEV, generator=g)
+    dep = torch.rand((2, 1, 48, 80), device=DEV, generator=g) * 10 * (torch.rand((2, 1, 48, 80), device=DEV,
+                                                                                   generator=g) < 0.05)
+    wide = torch.zeros((2, 1, 48, 160), device=DEV)
+    wide[..., ::2] = dep
+    with torch.no_grad():
+        fe1, id_fd1, oa_fd1, cf_fd1 = m._decoder({"rgb": rgb, "dep": dep})
+        ref = m._forward_fused(fe1, id_fd1, oa_fd1, cf_fd1, dep)
+        strided = m._forward_fused(fe1, id_fd1, oa_fd1, cf_fd1, wide[..., ::2])
+        f64 = m._forward_fused(fe1, id_fd1, oa_fd1, cf_fd1, dep.double())
+    for o in (strided, f64):
+        for k in ("pred", "aff", "confidence"):
+            assert torch.equal(o[k], ref[k]), k
+
+
+def test_replica_does_not_use_the_head_cache():
+    """DataParallel replicas share the module's __dict__ (so its packed-weight cache) but
+    hold fresh parameter copies: they pack per call."""
+    import types
+    from nlspn_eccv20_amd import NLSPNModel
+    args = types.SimpleNamespace(prop_kernel=3, affinity="TGASS", affinity_gamma=0.5, prop_time=6,
+                                 preserve_input=True, always_clip=False, conf_prop=True, offset=True,
+                                 network="resnet18", from_scratch=True, zero_init_aff=False, use_GRU=False,
+                                 use_S2D=False, GRU_hidden_dim=8, GRU_input_dim=8, lr=1e-3, max_depth=10.0,
+                                 patch_height=48, patch_width=80, model_name="NLSPN")
+    m = NLSPNModel(args).to(DEV).eval()
+    assert m._head_cache() is m._head_weights
+    rep = torch.nn.parallel.replicate(m, [0], detach=True)[0]
+    assert getattr(rep, "_is_replica", False) and rep._head_cache() is None

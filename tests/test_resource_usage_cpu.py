@@ -26,11 +26,11 @@ HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # checked on the kernel's device assembly, so a spill cannot come back into it silently.
 RESIDENT_SCRATCH_CAP = 64         # bytes per lane, single-group builds (setup slots)
 RESIDENT_SCRATCH_CAP_GROUPS = 192  # bytes per lane, GROUPS builds
-RESIDENT_LOOP_RELOADS = 2         # scratch instructions inside the iteration loop, per instantiation
+RESIDENT_LOOP_RELOADS = 0         # scratch instructions inside the iteration loop, per instantiation
 
 
 def _groups(name):
-    return name.endswith("ELb1EEEvNS_7ResArgsE")
+    return "ELb1E" in name
 
 
 _FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize"]
