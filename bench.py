@@ -298,9 +298,45 @@ def backward_timing(inputs, cfg, steps):
     torch.cuda.synchronize()
     fb = e[0].elapsed_time(e[1]) / steps
     fo = e[2].elapsed_time(e[3]) / steps
-    return {"ms_fwd_bwd_per_step": round(fb, 4), "ms_fwd_per_step": round(fo, 4),
-            "ms_bwd_per_iter": round((fb - fo) / cfg["T"], 5), "steps": steps,
-            "note": "eager autograd (not graph-replayed); bwd = fwd+bwd - fwd"}
+    out = {"ms_fwd_bwd_per_step": round(fb, 4), "ms_fwd_per_step": round(fo, 4),
+           "ms_bwd_per_iter": round((fb - fo) / cfg["T"], 5), "steps": steps,
+           "note": "eager autograd; bwd = fwd+bwd - fwd. graph: the same training step and forward captured "
+                   "into hipGraphs (torch.cuda.graph, whole step incl. autograd backward) and replayed"}
+    try:  # graph-replayed: no host launch gaps between the backward's per-iteration kernels
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                for t in (pi, cf, oa, g):
+                    t.grad = None
+                train_step()
+        torch.cuda.current_stream().wait_stream(side)
+        for t in (pi, cf, oa, g):
+            t.grad = None
+        gtrain, gfwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gtrain):
+            train_step()
+        with torch.no_grad(), torch.cuda.graph(gfwd):
+            fwd()
+        for gr in (gtrain, gfwd):
+            gr.replay()
+        torch.cuda.synchronize()
+        e[0].record()
+        for _ in range(steps):
+            gtrain.replay()
+        e[1].record()
+        e[2].record()
+        for _ in range(steps):
+            gfwd.replay()
+        e[3].record()
+        torch.cuda.synchronize()
+        fbg = e[0].elapsed_time(e[1]) / steps
+        fog = e[2].elapsed_time(e[3]) / steps
+        out.update({"ms_fwd_bwd_per_step_graph": round(fbg, 4), "ms_fwd_per_step_graph": round(fog, 4),
+                    "ms_bwd_per_iter_graph": round((fbg - fog) / cfg["T"], 5)})
+    except Exception as ex:  # noqa: BLE001  (report, do not fail the bench line)
+        out["graph_error"] = f"{type(ex).__name__}: {ex}"[:300]
+    return out
 
 
 def gru_section_timing(inputs, cfg, steps, dev):

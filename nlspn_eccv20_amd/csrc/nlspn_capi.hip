@@ -196,7 +196,9 @@ int launch(const StepLaunch &L, StepArgs &a, hipStream_t s, hipEvent_t e0 = null
 // part's quads fit one workgroup and its window fits LDS; otherwise the T-1
 // per-iteration launches run.  NLSPN_RESIDENT=0 in the environment forces the
 // per-iteration launches (A/B measurement).
-constexpr size_t kSyncBytes = 4096;  // progress words + abort word (nlspn_workspace_bytes)
+// the resident kernel's sync lines (nlspn_resident.h kResLine): the abort word's line and
+// one 128-B line per part, up to 512 parts (nlspn_workspace_bytes)
+constexpr size_t kSyncBytes = (1 + 512) * 4 * kResLine;
 
 int device_cus() {
     static int cached[64] = {0};
@@ -414,7 +416,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const int ng = (B + S.Bg - 1) / S.Bg;
     if (ng > kResMaxGroups) return false;
     const unsigned G = (unsigned)(S.Bg * S.gy * S.gx);
-    if ((G + 1) * 4 > kSyncBytes) return false;
+    if ((size_t)(G + 1) * 4 * kResLine > kSyncBytes) return false;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded)
     const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt,
@@ -423,12 +425,19 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false) : res_fn<__half>(S.nt, false);
     P.block = (unsigned)S.nt;
     P.lds = lds;
-    P.sync_bytes = ((G + 1) * 4 + 15) / 16 * 16;
+    P.sync_bytes = (size_t)(G + 1) * 4 * kResLine;
     P.ngroups = ng;
     DevState *ds = dev_state();
     unsigned dbg = 0;
     if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
     const int K = 8;
+    // Same-XCD hand-offs in the XCD's L2 (kResL2, nlspn_resident.h): possible where every
+    // image plane of every iteration starts and ends on a 128-B line (no line is shared
+    // by two images), not with the fused prologue; NLSPN_RES_L2=0 (A/B) keeps every
+    // hand-off write-through
+    const char *l2env = getenv("NLSPN_RES_L2");
+    const bool l2ok = !(l2env && l2env[0] == '0') && !F && ((long long)HW * (long long)es) % 128 == 0 &&
+                      aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
     for (int k = 0; k < ng; ++k) {
         const long long b0 = (long long)k * S.Bg;
         const int Bk = (int)std::min<long long>(S.Bg, B - b0);
@@ -441,7 +450,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          at(aff_norm, b0 * (K + 1) * HW), at(off_raw, b0 * off_bs),
                          const_cast<void *>(at(pred_inter, b0 * HW)), const_cast<void *>(at(pred, b0 * HW)),
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
-                         Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)), flags, dbg};
+                         Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)),
+                         flags | (l2ok ? kResL2 : 0u), dbg};
         if (F) {
             ResArgs &r = P.a[k];
             r.flags |= kResFirst;

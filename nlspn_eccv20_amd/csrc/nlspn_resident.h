@@ -125,6 +125,11 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 constexpr unsigned kResFirst = 0x200u;            // ResArgs::flags: iteration 1 + the prologue in this launch
+constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
+// The sync workspace: one 128-B line per word group — [0] the abort word, then per part
+// i (blockIdx) the line kResLine * (1 + i) holding its progress word and (word + 1) its
+// XCC id + 1.  No two parts share a line, so a line is only ever written from one XCD.
+constexpr int kResLine = 32;
 
 // Band i of n over a length L owns [i*L/n, (i+1)*L/n); owner(v) is the largest i
 // with floor(i*L/n) <= v.
@@ -272,6 +277,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                                    (size_t)blockIdx.x * a.T * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
     const bool active = tid < nown;
+    // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned, not fused): every
+    // part publishes the XCC it runs on; if all parts of its image share one, the image's
+    // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed.
+    const bool l2try = (a.flags & kResL2) != 0 && !fused;
+    unsigned xcc_self = 0;
+    if (l2try) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        xcc_self = (x & 0xfu) + 1u;
+        if (grp == 0 && tid == 0)
+            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xcc_self, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
     if (active) {
@@ -500,6 +518,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // vmcnt order, so polling from wave 0 added the store's round trip to every wait
     // (same-box A/B: C2 134.0k vs 124.1k iters/s, trace wait 0.96 vs 1.56 us)
     const int pwave = (nown - 1) >> 6;
+    bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in the first iteration)
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     for (int t = t0; t < a.T; ++t) {
         unsigned long long *trace = ((a.dbg & 8u) && t > 0) ? reinterpret_cast<unsigned long long *>(a.pred) +
@@ -508,6 +527,26 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         const bool first = t == 0;  // fused iteration 1: f = p0 * conf' from the raw inputs
         const T *p_in = first ? static_cast<const T *>(a.pinit) + b * HW : p_all + (size_t)(t - 1) * a.tstride + b * HW;
         const rsrc_t rp = make_rsrc(p_in);
+        // ---- a launch's first iteration: the hand-off mode of this image (all its parts
+        // on this part's XCC: L2), decided from the published XCC ids, identically by
+        // every part of the image; its stores at the end of this iteration use it
+        if (t == t0 && (tid >> 6) == pwave) {
+            bool same = l2try, fail = false;
+            unsigned spins = 0;
+            for (int base = 0; base < nparts && same && !fail; base += 64) {
+                const int jj = base + lane;
+                gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
+                unsigned v;
+                for (;;) {
+                    v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(v != 0u)) break;
+                    if (++spins > kResSpinLimit) { fail = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                same = same && __all(v == xcc_self);
+            }
+            if (lane == 0) ctl[5] = same && !fail ? 1 : 0;
+        }
         // ---- wait until every part this one reads has finished iteration t-1
         if (t > t0 && (tid >> 6) == pwave && !(a.dbg & 1u)) {
             unsigned spins = 0;
@@ -521,7 +560,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 // so a spin is ONE memory round trip (a separate abort load per spin, issued
                 // after the ballot, doubled the poll period)
                 const bool spare = base + 64 > ndep;
-                gu32 *wp = d < ndep ? &sync[1 + xcd_unmap(bl * nparts + jj, G)] : &sync[0];
+                gu32 *wp = d < ndep ? &sync[kResLine * (1 + xcd_unmap(bl * nparts + jj, G))] : &sync[0];
                 for (;;) {
                     const unsigned v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (__all(d >= ndep || v >= need)) break;
@@ -545,6 +584,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // keep draining under its staging and taps, until its publish
         if (t > t0) __syncthreads();
         else lds_barrier();
+        if (t == t0) l2 = __builtin_amdgcn_readfirstlane(ctl[5]) != 0;
         if (ctl[0]) {  // aborted: NaN in every plane this part has not written (this group's
                        // remaining iterations, every later group's), then exit
             if (active) {
@@ -756,7 +796,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 fin[e] = clip ? vv : clamp0(vv);  // :375-377
             }
             T *p_out = p_out_all + (size_t)t * a.tstride + b * HW;
-            ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);
+            if (l2) ResVec<T>::template store<0>(make_rsrc(p_out), vpix, 0u, o);  // kept in the XCD's L2
+            else ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
 #pragma unroll
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1 && !(a.dbg & 8u))
@@ -767,9 +808,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0)
-            __hip_atomic_store(&sync[1 + blockIdx.x], epoch + (unsigned)t + 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            gu32 *pw = &sync[kResLine * (1 + blockIdx.x)];
+            if (l2)  // same-XCD consumers only: a plain store, the line stays in the XCD's L2
+                __hip_atomic_store(pw, epoch + (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                __hip_atomic_store(pw, epoch + (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if constexpr (ES == 2) {
             // fused, fp16: iteration 1 used the normalised affinity unrounded (as step 1
             // does); the later iterations use it as stored (aff_out), reference weight

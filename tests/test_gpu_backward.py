@@ -134,3 +134,39 @@ def test_packed_head_gradient_equals_separate_slices(B, H, W, kernel, affinity):
         torch.cuda.synchronize()
         grads.append(oa.grad if packed else torch.cat([off.grad, aff.grad], 1))
     torch.testing.assert_close(grads[0], grads[1], rtol=1e-5, atol=1e-6)
+
+
+def test_training_step_graph_capture_matches_eager():
+    """The whole training step of the section (forward + autograd backward) captured into
+    a hipGraph (torch.cuda.graph) and replayed gives the eager gradients (bench.py's
+    graph-replayed backward timing runs exactly this)."""
+    B, H, W, K = 2, 48, 64, 8
+    s = synth(B, H, W, K, seed=11, density=0.05)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(DEV)  # noqa: E731
+    dep = t(s["dep"])
+    leaves = lambda: (t(s["pred_init"]).requires_grad_(True), t(s["conf"]).requires_grad_(True),  # noqa: E731
+                      t(s["off_aff"]).requires_grad_(True), torch.tensor([4.0], device=DEV, requires_grad=True))
+    gp = torch.randn((B, 1, H, W), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+
+    def step(pi, cf, oa, g):
+        o = propagate(pi, dep, cf, oa[:, 2 * K:], oa[:, :2 * K], g, prop_time=6)
+        torch.autograd.backward(o["pred"], gp)
+
+    ref = leaves()
+    step(*ref)
+    cap = leaves()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step(*cap)
+    torch.cuda.current_stream().wait_stream(side)
+    for x in cap:
+        x.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step(*cap)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    for x, y, n in zip(ref, cap, ("pred_init", "conf", "off_aff", "gamma")):
+        assert rel(y.grad.cpu().numpy(), x.grad.cpu().numpy()) <= 1e-6, n
