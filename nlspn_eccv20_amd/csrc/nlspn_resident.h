@@ -321,20 +321,23 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (has_conf)
             ResVec<T>::template load<0>(
                 make_rsrc(static_cast<const T *>(fused ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
-        if (fused) {
-            // step 1's prologue for the own quad (nlspn_step.h FIRST): the output-dict
-            // offsets (_off_insert, streamed: never re-read), the normalised affinity
-            // (_affinity_normalization + _aff_insert) and, below, conf'
-            if (active && a.off_out) {
-                const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
-                const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        // The output-dict offsets (_off_insert, nlspnmodel.py:324; streamed, never re-read)
+        // from the raw offsets just loaded, with the fused prologue.  (Writing them here in
+        // place of step 1 was measured slower: the 40 MB store burst delays the setup's
+        // invariant loads by 9 us where step 1 saves 6, profiles/r03/ab_offout_v1_*.txt.)
+        if (fused && active && a.off_out) {
+            const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
+            const float z[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int c = 0; c < K + 1; ++c) {
-                    const int k = c < REF ? c : c - 1;
-                    ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
-                    ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
-                }
+            for (int c = 0; c < K + 1; ++c) {
+                const int k = c < REF ? c : c - 1;
+                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
+                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
             }
+        }
+        if (fused) {
+            // step 1's prologue for the own quad (nlspn_step.h FIRST): the normalised
+            // affinity (_affinity_normalization + _aff_insert) and, below, conf'
             normalize_taps<K, 4>(ak, aref, a.kind, *a.gamma);
             if (active) {
                 const rsrc_t rao = make_rsrc(static_cast<T *>(const_cast<void *>(a.aff)) + (long long)b * (K + 1) * HW);

@@ -104,12 +104,20 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// fp16-storage offset steps: at least this many waves per SIMD (80 VGPRs), so that the
+// tap arithmetic of some waves overlaps the plane loads of others
+#ifndef NLSPN_STEP_F16_WAVES
+#define NLSPN_STEP_F16_WAVES 6
+#endif
+constexpr int kStepF16Waves = NLSPN_STEP_F16_WAVES;
+
 // KH x KW taps; TH x TW tile; PX px per thread; window radii RY/RX; SV = staging
 // vector width (4 requires W % 4 == 0 and RX % 4 == 0); PRE = issue every tap's
 // planes before the staging barrier (else inside pass A); FIRST = fused prologue.
 template <typename T, int KH, int KW, int TH, int TW, int PX, int RY, int RX, int SV, bool OFFSET, bool PRE,
           bool FIRST>
-__global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
+__global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FIRST && PX == 1 && SV == 4 && KH * KW <= 17) ? kStepF16Waves : 1)
+    prop_step_kernel(StepArgs a) {
     constexpr int NT = TH * TW / PX;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
     constexpr int PH = (KH - 1) / 2, PW = (KW - 1) / 2;
@@ -174,26 +182,49 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     }
 
     // ---- 2. streamed per-pixel loads: K affinity planes, 2K offset planes, dep [, conf].
-    float av[PRE ? K : 1][PX];
-    float dh[PRE ? K : 1][PX], dw[PRE ? K : 1][PX];
+    // MIX (fp16 storage, one pixel per lane): the affinity and offset planes stay fp16 in
+    // registers and enter the arithmetic through v_fma_mix_f32 (f16 operands converted
+    // exactly inside the instruction): x + y as fma(x, 1, y) and col = v * a as fma(v, a, 0)
+    // — the same roundings, and col's zero sign never reaches the accumulator (it starts
+    // at +0) — so 3 VALU per tap fewer than converting first.
+#ifndef NLSPN_STEP_NOMIX
+    constexpr bool MIX = sizeof(T) == 2 && PX == 1 && OFFSET && PRE && !FIRST;
+#else
+    constexpr bool MIX = false;  // A/B builds only
+#endif
+    using PT = typename std::conditional<MIX, _Float16, float>::type;
+    PT av[PRE ? K : 1][PX];
+    PT dh[PRE ? K : 1][PX], dw[PRE ? K : 1][PX];
     float dv[PX], cv[PX];
 #pragma unroll
     for (int p = 0; p < PX; ++p) dv[p] = cv[p] = 0.f;
     const rsrc_t ra = make_rsrc(static_cast<const T *>(a.aff) + b * a.aff_bs);
     const rsrc_t ro = make_rsrc(OFFSET ? static_cast<const T *>(a.off) + b * a.off_bs : static_cast<const T *>(a.aff));
+    auto load_pt = [&](rsrc_t r, unsigned so, PT (&dst)[PX]) {
+        if constexpr (MIX) {
+            dst[0] = __builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vpix, so, 0));
+        } else {
+            float f[PX];
+            BVec<T, PX>::load(r, vpix, so, f);
+#pragma unroll
+            for (int p = 0; p < PX; ++p) dst[p] = f[p];
+        }
+    };
     if (PRE) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             // FIRST: raw affinity (K planes); otherwise the normalised (K+1)-plane layout
             const unsigned ap = FIRST ? (unsigned)k : (unsigned)(k < REF ? k : k + 1);
-            BVec<T, PX>::load(ra, vpix, ap * plane_bytes, av[PRE ? k : 0]);
+            load_pt(ra, ap * plane_bytes, av[PRE ? k : 0]);
             if (OFFSET) {
                 const unsigned c = a.off_raw ? k : (k < REF ? k : k + 1);
-                BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, dh[PRE ? k : 0]);
-                BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, dw[PRE ? k : 0]);
+                load_pt(ro, (2 * c) * plane_bytes, dh[PRE ? k : 0]);
+                load_pt(ro, (2 * c + 1) * plane_bytes, dw[PRE ? k : 0]);
             }
         }
     }
+    float one = 1.0f;  // opaque 1: fma(x, one, y) stays an fma (mixed precision), not an add
+    asm volatile("" : "+v"(one));
     if (preserve) BVec<T, PX>::load(rd, vpix, 0u, dv);
     if (FIRST && has_conf) BVec<T, PX>::load(rc, vpix, 0u, cv);
 
@@ -221,7 +252,7 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
 
     // ---- FIRST: the prologue's per-pixel outputs (normalised affinity, conf', offsets)
     float fref_a[PX];  // FIRST: reference-tap weight from the normalisation (== 1 - sum, same order)
-    if (FIRST) {
+    if constexpr (FIRST) {
         normalize_taps<K, PX>(av, fref_a, a.kind, *a.gamma);
         const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + b * (K + 1) * HW);
 #pragma unroll
@@ -286,64 +317,60 @@ __global__ void __launch_bounds__(TH * TW / PX) prop_step_kernel(StepArgs a) {
     uint32_t fb[NFB];
 #pragma unroll
     for (int q = 0; q < NFB; ++q) fb[q] = 0u;
-    // pass A, instantiated for edge tiles (the h == -1 / w == -1 fix-up) and the rest, so
-    // the tile-uniform choice is one branch outside the tap loop
-    auto pass_a = [&](auto edge) {
-        constexpr bool EDGE = decltype(edge)::value;
-    #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int t = k < REF ? k : k + 1;
-            const int i = t / KW, j = t % KW;
-            float ak[PX], tdh[PX], tdw[PX];
-            if (PRE) {
-    #pragma unroll
-                for (int p = 0; p < PX; ++p) {
-                    ak[p] = av[PRE ? k : 0][p];
-                    tdh[p] = dh[PRE ? k : 0][p];
-                    tdw[p] = dw[PRE ? k : 0][p];
-                }
-            } else {
-                BVec<T, PX>::load(ra, vpix, (unsigned)t * plane_bytes, ak);
-                if (OFFSET) {
-                    const unsigned c = a.off_raw ? k : t;
-                    BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, tdh);
-                    BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, tdw);
-                }
-            }
-    #pragma unroll
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int t = k < REF ? k : k + 1;
+        const int i = t / KW, j = t % KW;
+        PT ak[PX], tdh[PX], tdw[PX];
+        if (PRE) {
+#pragma unroll
             for (int p = 0; p < PX; ++p) {
-                asum[p] += ak[p];
-                if (!OFFSET) {
-                    col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
-                    continue;
-                }
-                // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
-                // the tap's base coordinates as exact float sums of small integers (one add per
-                // tap instead of an integer add and a convert): the same values as
-                // (float)(y - PH + i) and (float)(xb + p - PW + j)
-                const float h_im = (i == 0 ? yb_f : yb_f + (float)i) + tdh[p];  // yb_f + 0 == yb_f: never -0
-                const float w_im = (xb_f + (float)(p + j)) + tdw[p];
-                float v = 0.f;
-                if (h_im >= lo_h && h_im < hi_h && w_im >= lo_w && w_im < hi_w) {
-                    // valid and in the window: (float)h_low == fh, so h_im - fh is the
-                    // reference's h_im - (float)h_low (.cuh:35-36)
-                    const float fh = floorf(h_im), fw = floorf(w_im);
-                    const float lh = h_im - fh, lw = w_im - fw;
-                    const float hh = 1.f - lh, hw = 1.f - lw;
-                    const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
-                    const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
-                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
-                    if (EDGE && (h_im == -1.f || w_im == -1.f)) v = 0.f;  // invalid: val = 0
-                } else {
-                    fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);  // pass B
-                }
-                col[k][p] = v * ak[p];  // .cuh:189 col = val * mask
+                ak[p] = av[PRE ? k : 0][p];
+                tdh[p] = dh[PRE ? k : 0][p];
+                tdw[p] = dw[PRE ? k : 0][p];
+            }
+        } else if constexpr (!MIX) {
+            BVec<T, PX>::load(ra, vpix, (unsigned)t * plane_bytes, ak);
+            if (OFFSET) {
+                const unsigned c = a.off_raw ? k : t;
+                BVec<T, PX>::load(ro, vpix, (2 * c) * plane_bytes, tdh);
+                BVec<T, PX>::load(ro, vpix, (2 * c + 1) * plane_bytes, tdw);
             }
         }
-    };
-    if (edge_tile) pass_a(std::true_type{});
-    else pass_a(std::false_type{});
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+            if constexpr (MIX) asum[p] = __builtin_fmaf((float)ak[p], one, asum[p]);
+            else asum[p] += ak[p];
+            if (!OFFSET) {
+                col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
+                continue;
+            }
+            // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
+            // the tap's base coordinates as exact float sums of small integers (one add per
+            // tap instead of an integer add and a convert): the same values as
+            // (float)(y - PH + i) and (float)(xb + p - PW + j)
+            const float hb = i == 0 ? yb_f : yb_f + (float)i;  // yb_f + 0 == yb_f: never -0
+            const float wb = xb_f + (float)(p + j);
+            const float h_im = MIX ? __builtin_fmaf((float)tdh[p], one, hb) : hb + (float)tdh[p];
+            const float w_im = MIX ? __builtin_fmaf((float)tdw[p], one, wb) : wb + (float)tdw[p];
+            float v = 0.f;
+            if (h_im >= lo_h && h_im < hi_h && w_im >= lo_w && w_im < hi_w) {
+                // valid and in the window: (float)h_low == fh, so h_im - fh is the
+                // reference's h_im - (float)h_low (.cuh:35-36)
+                const float fh = floorf(h_im), fw = floorf(w_im);
+                const float lh = h_im - fh, lw = w_im - fw;
+                const float hh = 1.f - lh, hw = 1.f - lw;
+                const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
+                const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
+                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
+                if (edge_tile && (h_im == -1.f || w_im == -1.f)) v = 0.f;  // invalid: val = 0
+            } else {
+                fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);  // pass B
+            }
+            col[k][p] = MIX ? __builtin_fmaf(v, (float)ak[p], 0.f) : v * (float)ak[p];  // .cuh:189 col = val * mask
+        }
+    }
     uint32_t any_fb = 0u;
 #pragma unroll
     for (int q = 0; q < NFB; ++q) any_fb |= fb[q];
