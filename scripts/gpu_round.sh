@@ -5,7 +5,7 @@
 # usage: scripts/gpu_round.sh [TAG]   (outputs under gpurun_out/round_TAG)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r02}
+TAG=${1:-r03}
 O=$R/gpurun_out/round_$TAG
 mkdir -p $O
 cd $R
@@ -21,13 +21,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o bench --output
     python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru > $O/stats.log 2>&1 || exit 1
 # kernel stats per config (kernels are shared between configs, so the default run's
 # averages mix them): each bench config alone, for the roofline cross-check
-for CFG in nyu kitti nyu_k16; do
+for CFG in nyu kitti nyu_k16 nyu_b1; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_$CFG -o bench --output-format csv -- \
       python3 $R/bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru --no-heads \
       --no-extra-configs > $O/stats_$CFG.log 2>&1 || exit 1
 done
 # PMC HBM traffic, one config per pass pair (kernels are shared between configs)
-for CFG in nyu kitti nyu_k16; do
+for CFG in nyu kitti nyu_k16 nyu_b1; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace -d $O/pmc_${CFG}_$C -o run --output-format csv -- \
         python3 $R/bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-backward --no-gru \
