@@ -104,6 +104,26 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// a (f16, low half) * b + c in f32 with one rounding (v_fma_mix_f32; the f16 operand is
+// converted exactly inside the instruction).  Inline asm: left to itself the SLP
+// vectoriser pairs two of these into two converts + a v_pk_fma_f32.
+__device__ __forceinline__ float fma_mix_lo(_Float16 a, float b, float c) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// packed f32 (VOP3P: per-lane IEEE, bit-identical to the scalar ops) with element E of
+// the first / second operand broadcast to both lanes
+template <int E>
+__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 b, f32x2 c) {
+    return __builtin_elementwise_fma(__builtin_shufflevector(a, a, E, E), b, c);
+}
+template <int E>
+__device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 b) {
+    return a * __builtin_shufflevector(b, b, E, E);
+}
+constexpr f32x2 kNegOne = {-1.f, 1.f}, kOneZero = {1.f, 0.f};
+
 // fp16-storage offset steps: at least this many waves per SIMD (80 VGPRs), so that the
 // tap arithmetic of some waves overlaps the plane loads of others
 #ifndef NLSPN_STEP_F16_WAVES
@@ -132,7 +152,9 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     constexpr int NV = WH * WV;                  // staging vectors per window
     constexpr int SIT = (NV + NT - 1) / NT;      // staging vectors per thread
     constexpr unsigned ES = sizeof(T);
-    __shared__ __attribute__((aligned(16))) float win[WH * WW];
+    constexpr int NW = NT / 64;
+    // the window, then one word per wave: "this wave staged a non-finite f" (edge tiles)
+    __shared__ __attribute__((aligned(16))) float win[WH * WW + NW];
 
     const int H = a.H, W = a.W;
     const long long HW = (long long)H * W;
@@ -162,9 +184,29 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     const unsigned vpix = pix * ES;            // per-lane byte offset, shared by every plane
     const unsigned plane_bytes = (unsigned)HW * ES;
 
-    // ---- 1. staging loads (first): the window's p, conf [, dep], clamped addresses
+    // MIX (fp16 storage, one pixel per lane, offset steps after the first): the plane values
+    // stay fp16 in registers and enter the arithmetic through v_fma_mix_f32 (f16 operands
+    // converted exactly inside the instruction); see the streamed loads below.
+#ifndef NLSPN_STEP_NOMIX
+    constexpr bool MIX = sizeof(T) == 2 && PX == 1 && OFFSET && PRE && !FIRST;
+#else
+    constexpr bool MIX = false;  // A/B builds only
+#endif
+    // MIX staging (SV = 4): cells outside the image load from an out-of-range buffer offset,
+    // which the buffer unit returns as zeros (= the zero padding, no select per cell), and
+    // f = p * conf' is one v_fma_mix_f32 (an f16 x f16 product is exact in f32: fma(p, c, 0)
+    // == p * c but for the sign of a zero product, which never reaches a result — the
+    // bilinear sums and the tap accumulator start at +0).
+#ifndef NLSPN_STEP_NOMIXS
+    constexpr bool MIXS = MIX && SV == 4;
+#else
+    constexpr bool MIXS = false;  // A/B builds only
+#endif
+    constexpr unsigned kOOB = 0x80000000u;  // >= num_records (make_rsrc): reads as 0
     float sp[SIT][SV], sc[SIT][SV], sd[FIRST ? SIT : 1][SV];
+    f16x4 sp16[MIXS ? SIT : 1], sc16[MIXS ? SIT : 1];
     bool sin[SIT];
+    // ---- 1. staging loads (first): the window's p, conf [, dep], clamped addresses
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
         const int i = threadIdx.x + it * NT;
@@ -173,6 +215,12 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
         int gy = wy0 + r, gx = wx0 + c;
         if (OFFSET) sin[it] = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;  // zero padding outside
         else sin[it] = i < NV;                                                   // replicate padding
+        if constexpr (MIXS) {
+            const unsigned q = sin[it] ? (unsigned)(gy * W + gx) * ES : kOOB;
+            sp16[it] = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(rp, q, 0u, 0));
+            if (has_conf) sc16[it] = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(rc, q, 0u, 0));
+            continue;
+        }
         gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
         gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
         const unsigned q = (unsigned)(gy * W + gx) * ES;
@@ -182,16 +230,9 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     }
 
     // ---- 2. streamed per-pixel loads: K affinity planes, 2K offset planes, dep [, conf].
-    // MIX (fp16 storage, one pixel per lane): the affinity and offset planes stay fp16 in
-    // registers and enter the arithmetic through v_fma_mix_f32 (f16 operands converted
-    // exactly inside the instruction): x + y as fma(x, 1, y) and col = v * a as fma(v, a, 0)
-    // — the same roundings, and col's zero sign never reaches the accumulator (it starts
-    // at +0) — so 3 VALU per tap fewer than converting first.
-#ifndef NLSPN_STEP_NOMIX
-    constexpr bool MIX = sizeof(T) == 2 && PX == 1 && OFFSET && PRE && !FIRST;
-#else
-    constexpr bool MIX = false;  // A/B builds only
-#endif
+    // MIX: the affinity and offset planes stay fp16: x + y as fma(x, 1, y) and col = v * a
+    // as fma(v, a, 0) — the same roundings, and col's zero sign never reaches the
+    // accumulator (it starts at +0) — so 3 VALU per tap fewer than converting first.
     using PT = typename std::conditional<MIX, _Float16, float>::type;
     PT av[PRE ? K : 1][PX];
     PT dh[PRE ? K : 1][PX], dw[PRE ? K : 1][PX];
@@ -229,10 +270,48 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     if (FIRST && has_conf) BVec<T, PX>::load(rc, vpix, 0u, cv);
 
     // ---- 3. finish staging into LDS (waits for the staging loads only)
+    // Edge tiles (window above or left of the image) note whether the window holds a
+    // non-finite f: only then can an invalid tap at exactly h == -1 / w == -1 (0 * f over
+    // the in-image row / column) differ from the reference's val = 0 (pass B below).
+    const bool edge_tile = wy0 < 0 || wx0 < 0;
+    bool nonfin = false;
+    const auto stage_store = [&](int it, const float (&v)[SV]) {
+        if (edge_tile) {
 #pragma unroll
-    for (int it = 0; it < SIT; ++it) {
+            for (int e = 0; e < SV; ++e) nonfin |= !__builtin_isfinite(v[e]);
+        }
         const int i = threadIdx.x + it * NT;
-        if (i < NV) {
+        const int r = i / WV, c = (i - r * WV) * SV;
+        if constexpr (SV == 4)
+            *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
+        else
+            win[r * WW + c] = v[0];
+    };
+    if constexpr (MIXS) {  // out-of-image cells loaded as zeros: 0 * 0 = +0
+        // two loops under the uniform has_conf branch (one select per cell otherwise)
+        if (has_conf) {
+#pragma unroll
+            for (int it = 0; it < SIT; ++it) {
+                if (threadIdx.x + it * NT >= NV) continue;
+                float v[SV];
+#pragma unroll
+                for (int e = 0; e < SV; ++e) v[e] = __builtin_fmaf((float)sp16[it][e], (float)sc16[it][e], 0.0f);
+                stage_store(it, v);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < SIT; ++it) {
+                if (threadIdx.x + it * NT >= NV) continue;
+                float v[SV];
+#pragma unroll
+                for (int e = 0; e < SV; ++e) v[e] = (float)sp16[it][e];
+                stage_store(it, v);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < SIT; ++it) {
+            if (threadIdx.x + it * NT >= NV) continue;
             float v[SV];
 #pragma unroll
             for (int e = 0; e < SV; ++e) {
@@ -240,15 +319,20 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
                                               FIRST && preserve ? sd[FIRST ? it : 0][e] : 0.f, has_conf, preserve, clip);
                 v[e] = sin[it] ? f : 0.f;
             }
-            const int r = i / WV, c = (i - r * WV) * SV;
-            if constexpr (SV == 4)
-                *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
-            else
-                win[r * WW + c] = v[0];
+            stage_store(it, v);
         }
+    }
+    if (edge_tile) {
+        const bool wnf = __builtin_amdgcn_ballot_w64(nonfin) != 0;
+        if ((threadIdx.x & 63) == 0) win[WH * WW + threadIdx.x / 64] = wnf ? 1.f : 0.f;
     }
     lds_barrier();
     if (!active) return;  // no barrier below
+    bool edge_fix = false;  // tile-uniform
+    if (edge_tile) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) edge_fix |= win[WH * WW + w] != 0.f;
+    }
 
     // ---- FIRST: the prologue's per-pixel outputs (normalised affinity, conf', offsets)
     float fref_a[PX];  // FIRST: reference-tap weight from the normalisation (== 1 - sum, same order)
@@ -286,10 +370,11 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     // ---- 4. taps.  Pass A (LDS only, no divergent global loads, so the
     // compiler's vmcnt waits stay counted per tap): col[k] = bilinear * a_k for
     // every tap whose 2x2 footprint is inside the window (one range test; invalid taps
-    // there sample zeros, see lo_h below); taps outside it are flagged in `fb`.  Pass B
-    // (rare): flagged taps test validity (invalid: col = 0 * a stands) and the valid
-    // ones are sampled from L2/global with the reference's per-corner checks (their
-    // offsets re-read from cache).  Then
+    // there sample zeros, see lo_h below); a lane with a tap outside it sets `anyout`
+    // (a lane mask, no vector work per tap).  Pass B (rare): such lanes re-read their
+    // offsets from cache, skip the taps pass A served (the same test on the same values),
+    // test validity (invalid: col = 0 * a stands) and sample the valid ones from
+    // L2/global with the reference's per-corner checks.  Then
     // accumulate in tap index order with the reference tap (K/2) weighted
     // 1 - sum(others) (nlspnmodel.py:262-263): the reference's summation order,
     // whichever pass served a tap.  col = val * a then acc += col is the same
@@ -300,23 +385,44 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     const float Hf = (float)H, Wf = (float)W;
     const float yb_f = (float)(y - PH), xb_f = (float)(xb - PW);  // |values| < 2^24: exact
     // One range test per tap: the footprint rows floor(h), floor(h)+1 lie in the window iff
-    // wy0 <= h < wy0 + WH - 1 (likewise w).  The window holds zeros outside the image, so
+    // wy0 <= h < wy0 + WH - 1 (likewise w), tested as the bits of h - wy0 (one packed
+    // subtract for h and w) below those of WH - 1: a negative difference (sign bit), NaN
+    // and anything >= WH - 1 fail, and rounding can only fail a tap that is in range
+    // (pass B serves it exactly).  The window holds zeros outside the image, so
     // an INVALID tap (outside (-1, H) x (-1, W), .cuh:180) whose footprint is in the
     // window samples exactly +0 there — the reference's val = 0 — except at h == -1 or
     // w == -1 exactly, where the in-image row / column enters with weight 0 (0 * f, NaN
-    // for a non-finite f): tiles whose window reaches above or left of the image zero
-    // those taps explicitly (a tile-uniform branch).  A tap outside the window (or NaN)
-    // goes to pass B, which tests validity first.
-    const float lo_h = (float)wy0, hi_h = (float)(wy0 + WH - 1);
-    const float lo_w = (float)wx0, hi_w = (float)(wx0 + WW - 1);
-    const bool edge_tile = wy0 < 0 || wx0 < 0;
+    // for a non-finite f): when an edge tile's window holds a non-finite f (edge_fix,
+    // tile-uniform, from the staging) every lane runs pass B, which zeroes those taps —
+    // no per-tap test on the common path (an in-loop test costs 3 VALU per tap; a re-read
+    // fix-up after pass A measured 14 % slower at C5, profiles/r03/ab_step_ablation_v1.txt).
+    // A tap outside the window (or NaN) goes to pass B, which tests validity first.
+    const float lo_h = (float)wy0, lo_w = (float)wx0;
+    const f32x2 lo2 = {lo_h, lo_w};
+    constexpr unsigned kLimH = __builtin_bit_cast(unsigned, (float)(WH - 1));
+    constexpr unsigned kLimW = __builtin_bit_cast(unsigned, (float)(WW - 1));
     // window byte offset of the footprint's top-left cell, from the floors in exact float
     // arithmetic (small integers): 4 (floor(h) - wy0) WW + 4 (floor(w) - wx0)
     const float wofs = -4.f * (float)(wy0 * WW + wx0);
-    constexpr int NFB = (K * PX + 31) / 32;
-    uint32_t fb[NFB];
-#pragma unroll
-    for (int q = 0; q < NFB; ++q) fb[q] = 0u;
+    bool anyout = edge_fix;  // this lane has a tap outside the window (pass B)
+    f32x2 negone = kNegOne, onezero = kOneZero;  // loop-invariant registers (one SGPR operand per VOP3P)
+    asm volatile("" : "+s"(negone), "+v"(onezero));
+    const auto tap_coords = [&](int k, int p, PT dh_, PT dw_, float &h_im, float &w_im) {
+        const int t = k < REF ? k : k + 1;
+        const int i = t / KW, j = t % KW;
+        // modulated_deform_im2col_cuda.cuh:178-189: the tap's base coordinates as exact
+        // float sums of small integers (one add per tap instead of an integer add and a
+        // convert): the same values as (float)(y - PH + i) and (float)(xb + p - PW + j)
+        const float hb = i == 0 ? yb_f : yb_f + (float)i;  // yb_f + 0 == yb_f: never -0
+        const float wb = xb_f + (float)(p + j);
+        if constexpr (MIX) {
+            h_im = fma_mix_lo(dh_, one, hb);
+            w_im = fma_mix_lo(dw_, one, wb);
+        } else {
+            h_im = hb + (float)dh_;
+            w_im = wb + (float)dw_;
+        }
+    };
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int t = k < REF ? k : k + 1;
@@ -339,55 +445,86 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
         }
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
-            if constexpr (MIX) asum[p] = __builtin_fmaf((float)ak[p], one, asum[p]);
-            else asum[p] += ak[p];
+            if constexpr (MIX) {  // asum += a as one v_fma_mix_f32 (a * 1 + asum, a read as f16)
+                asum[p] = fma_mix_lo(ak[p], one, asum[p]);
+            } else {
+                asum[p] += ak[p];
+            }
             if (!OFFSET) {
                 col[k][p] = win[(ly + RY + i - 1) * WW + lx + p + RX + j - 1] * ak[p];
                 continue;
             }
-            // modulated_deform_im2col_cuda.cuh:178-189 + mdmcn_im2col_bilinear :24-54
-            // the tap's base coordinates as exact float sums of small integers (one add per
-            // tap instead of an integer add and a convert): the same values as
-            // (float)(y - PH + i) and (float)(xb + p - PW + j)
-            const float hb = i == 0 ? yb_f : yb_f + (float)i;  // yb_f + 0 == yb_f: never -0
-            const float wb = xb_f + (float)(p + j);
-            const float h_im = MIX ? __builtin_fmaf((float)tdh[p], one, hb) : hb + (float)tdh[p];
-            const float w_im = MIX ? __builtin_fmaf((float)tdw[p], one, wb) : wb + (float)tdw[p];
-            float v = 0.f;
-            if (h_im >= lo_h && h_im < hi_h && w_im >= lo_w && w_im < hi_w) {
-                // valid and in the window: (float)h_low == fh, so h_im - fh is the
-                // reference's h_im - (float)h_low (.cuh:35-36)
+            float h_im, w_im;
+            tap_coords(k, p, tdh[p], tdw[p], h_im, w_im);
+            const f32x2 hw2 = {h_im, w_im};
+            const f32x2 rel = hw2 - lo2;
+            const u32x2 rb = __builtin_bit_cast(u32x2, rel);  // whole-vector cast (see BVec's note)
+            const bool in = rb[0] < kLimH && rb[1] < kLimW;
+            anyout |= !in;
+#ifdef NLSPN_STEP_BRANCHFREE
+            float v;
+            {  // every lane samples (an out-of-window lane reads some LDS word), then selects
+                // mdmcn_im2col_bilinear (.cuh:24-54), in the window: (float)h_low == fh, so
+                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36); the (h, w)
+                // pairs and the weight / sample products in packed f32 (per-lane IEEE)
                 const float fh = floorf(h_im), fw = floorf(w_im);
-                const float lh = h_im - fh, lw = w_im - fw;
-                const float hh = 1.f - lh, hw = 1.f - lw;
+                const f32x2 l = hw2 - (f32x2){fh, fw};        // (lh, lw)
                 const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
                 const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
-                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
-                if (edge_tile && (h_im == -1.f || w_im == -1.f)) v = 0.f;  // invalid: val = 0
-            } else {
-                fb[(k * PX + p) >> 5] |= 1u << ((k * PX + p) & 31);  // pass B
+                // (hh, lh) and (hw, lw) as fma(l, (-1, 1), (1, 0)): 1 - l and l, one rounding each
+                const f32x2 hv = pk_fma_bcast<0>(l, negone, onezero);  // (hh, lh)
+                const f32x2 wv = pk_fma_bcast<1>(l, negone, onezero);  // (hw, lw)
+                const f32x2 w12 = pk_mul_bcast<0>(wv, hv), w34 = pk_mul_bcast<1>(wv, hv);  // (w1, w2), (w3, w4)
+                const f32x2 s01 = {s[0], s[1]}, s23 = {s[WW], s[WW + 1]};
+                const f32x2 p12 = w12 * s01, p34 = w34 * s23;
+                v = ((p12[0] + p12[1]) + p34[0]) + p34[1];
             }
+            v = in ? v : 0.f;
+#else
+            float v = 0.f;
+            if (in) {
+                // mdmcn_im2col_bilinear (.cuh:24-54), in the window: (float)h_low == fh, so
+                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36); the (h, w)
+                // pairs and the weight / sample products in packed f32 (per-lane IEEE)
+                const float fh = floorf(h_im), fw = floorf(w_im);
+                const f32x2 l = hw2 - (f32x2){fh, fw};        // (lh, lw)
+                const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
+                const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
+                // (hh, lh) and (hw, lw) as fma(l, (-1, 1), (1, 0)): 1 - l and l, one rounding each
+                const f32x2 hv = pk_fma_bcast<0>(l, negone, onezero);  // (hh, lh)
+                const f32x2 wv = pk_fma_bcast<1>(l, negone, onezero);  // (hw, lw)
+                const f32x2 w12 = pk_mul_bcast<0>(wv, hv), w34 = pk_mul_bcast<1>(wv, hv);  // (w1, w2), (w3, w4)
+                const f32x2 s01 = {s[0], s[1]}, s23 = {s[WW], s[WW + 1]};
+                const f32x2 p12 = w12 * s01, p34 = w34 * s23;
+                v = ((p12[0] + p12[1]) + p34[0]) + p34[1];
+            }
+#endif
             col[k][p] = MIX ? __builtin_fmaf(v, (float)ak[p], 0.f) : v * (float)ak[p];  // .cuh:189 col = val * mask
         }
     }
-    uint32_t any_fb = 0u;
-#pragma unroll
-    for (int q = 0; q < NFB; ++q) any_fb |= fb[q];
-    if (OFFSET && any_fb) {
+    if (OFFSET && anyout) {  // pass B: the lane's taps outside the window, offsets re-read
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = k < REF ? k : k + 1;
             const int i = t / KW, j = t % KW;
 #pragma unroll
             for (int p = 0; p < PX; ++p) {
-                if (!(fb[(k * PX + p) >> 5] & (1u << ((k * PX + p) & 31)))) continue;
                 const unsigned c = a.off_raw ? k : t;
                 float o1[1], a1[1];
                 BVec<T, 1>::load(ro, vpix + p * ES, (2 * c) * plane_bytes, o1);
                 const float h_im = (float)(y - PH + i) + o1[0];
                 BVec<T, 1>::load(ro, vpix + p * ES, (2 * c + 1) * plane_bytes, o1);
                 const float w_im = (float)(xb + p - PW + j) + o1[0];
+                if (edge_fix && (h_im == -1.f || w_im == -1.f)) {  // invalid (.cuh:180): val = 0
+                    if (FIRST) a1[0] = av[PRE ? k : 0][p];
+                    else BVec<T, 1>::load(ra, vpix + p * ES, (unsigned)t * plane_bytes, a1);
+                    col[k][p] = 0.f * a1[0];
+                    continue;
+                }
+                {  // served by pass A (the same test on the same values)
+                    const u32x2 rb = __builtin_bit_cast(u32x2, (f32x2){h_im, w_im} - lo2);
+                    if (rb[0] < kLimH && rb[1] < kLimW) continue;
+                }
                 // invalid (.cuh:180, NaN included): the reference's val = 0, already col = 0 * a above
                 if (!(h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf)) continue;
                 if (FIRST) a1[0] = av[PRE ? k : 0][p];  // normalised in registers above

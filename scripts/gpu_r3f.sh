@@ -1,0 +1,14 @@
+#!/bin/bash
+# Step-kernel VALU trim: parity (fp16 bit-exact step tests, exact -1 taps, the parity /
+# golden / resident suites), then a same-box A/B of the in-tree build vs the saved
+# round-3 base library on C5 / C2 / C3 / C1.
+set -o pipefail
+O=gpurun_out/r3f_$1; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_step_fp16.py tests/test_gpu_parity.py tests/test_offset_golden.py \
+    tests/test_gpu_heads_prologue.py tests/test_gpu_resident.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+    > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for CFG in nyu_k16 nyu kitti nyu_b1; do
+  AB_CONFIG=$CFG bash scripts/gpu_ab.sh cur=- base=nlspn_eccv20_amd/lib/ab/libnlspn_r3base.so > $O/ab_$CFG.txt 2>&1 || { cat $O/ab_$CFG.txt; exit 1; }
+  echo "== $CFG"; cat $O/ab_$CFG.txt
+done
