@@ -112,17 +112,6 @@ __device__ __forceinline__ float fma_mix_lo(_Float16 a, float b, float c) {
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-// packed f32 (VOP3P: per-lane IEEE, bit-identical to the scalar ops) with element E of
-// the first / second operand broadcast to both lanes
-template <int E>
-__device__ __forceinline__ f32x2 pk_fma_bcast(f32x2 a, f32x2 b, f32x2 c) {
-    return __builtin_elementwise_fma(__builtin_shufflevector(a, a, E, E), b, c);
-}
-template <int E>
-__device__ __forceinline__ f32x2 pk_mul_bcast(f32x2 a, f32x2 b) {
-    return a * __builtin_shufflevector(b, b, E, E);
-}
-constexpr f32x2 kNegOne = {-1.f, 1.f}, kOneZero = {1.f, 0.f};
 
 // fp16-storage offset steps: at least this many waves per SIMD (80 VGPRs), so that the
 // tap arithmetic of some waves overlaps the plane loads of others
@@ -385,8 +374,8 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     const float Hf = (float)H, Wf = (float)W;
     const float yb_f = (float)(y - PH), xb_f = (float)(xb - PW);  // |values| < 2^24: exact
     // One range test per tap: the footprint rows floor(h), floor(h)+1 lie in the window iff
-    // wy0 <= h < wy0 + WH - 1 (likewise w), tested as the bits of h - wy0 (one packed
-    // subtract for h and w) below those of WH - 1: a negative difference (sign bit), NaN
+    // wy0 <= h < wy0 + WH - 1 (likewise w), tested as the bits of h - wy0 (an unsigned
+    // compare) below those of WH - 1: a negative difference (sign bit), NaN
     // and anything >= WH - 1 fail, and rounding can only fail a tap that is in range
     // (pass B serves it exactly).  The window holds zeros outside the image, so
     // an INVALID tap (outside (-1, H) x (-1, W), .cuh:180) whose footprint is in the
@@ -398,15 +387,12 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     // fix-up after pass A measured 14 % slower at C5, profiles/r03/ab_step_ablation_v1.txt).
     // A tap outside the window (or NaN) goes to pass B, which tests validity first.
     const float lo_h = (float)wy0, lo_w = (float)wx0;
-    const f32x2 lo2 = {lo_h, lo_w};
     constexpr unsigned kLimH = __builtin_bit_cast(unsigned, (float)(WH - 1));
     constexpr unsigned kLimW = __builtin_bit_cast(unsigned, (float)(WW - 1));
     // window byte offset of the footprint's top-left cell, from the floors in exact float
     // arithmetic (small integers): 4 (floor(h) - wy0) WW + 4 (floor(w) - wx0)
     const float wofs = -4.f * (float)(wy0 * WW + wx0);
     bool anyout = edge_fix;  // this lane has a tap outside the window (pass B)
-    f32x2 negone = kNegOne, onezero = kOneZero;  // loop-invariant registers (one SGPR operand per VOP3P)
-    asm volatile("" : "+s"(negone), "+v"(onezero));
     const auto tap_coords = [&](int k, int p, PT dh_, PT dw_, float &h_im, float &w_im) {
         const int t = k < REF ? k : k + 1;
         const int i = t / KW, j = t % KW;
@@ -456,49 +442,22 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
             }
             float h_im, w_im;
             tap_coords(k, p, tdh[p], tdw[p], h_im, w_im);
-            const f32x2 hw2 = {h_im, w_im};
-            const f32x2 rel = hw2 - lo2;
-            const u32x2 rb = __builtin_bit_cast(u32x2, rel);  // whole-vector cast (see BVec's note)
-            const bool in = rb[0] < kLimH && rb[1] < kLimW;
+            const bool in = __builtin_bit_cast(unsigned, h_im - lo_h) < kLimH && __builtin_bit_cast(unsigned, w_im - lo_w) < kLimW;
             anyout |= !in;
-#ifdef NLSPN_STEP_BRANCHFREE
-            float v;
-            {  // every lane samples (an out-of-window lane reads some LDS word), then selects
-                // mdmcn_im2col_bilinear (.cuh:24-54), in the window: (float)h_low == fh, so
-                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36); the (h, w)
-                // pairs and the weight / sample products in packed f32 (per-lane IEEE)
-                const float fh = floorf(h_im), fw = floorf(w_im);
-                const f32x2 l = hw2 - (f32x2){fh, fw};        // (lh, lw)
-                const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
-                const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
-                // (hh, lh) and (hw, lw) as fma(l, (-1, 1), (1, 0)): 1 - l and l, one rounding each
-                const f32x2 hv = pk_fma_bcast<0>(l, negone, onezero);  // (hh, lh)
-                const f32x2 wv = pk_fma_bcast<1>(l, negone, onezero);  // (hw, lw)
-                const f32x2 w12 = pk_mul_bcast<0>(wv, hv), w34 = pk_mul_bcast<1>(wv, hv);  // (w1, w2), (w3, w4)
-                const f32x2 s01 = {s[0], s[1]}, s23 = {s[WW], s[WW + 1]};
-                const f32x2 p12 = w12 * s01, p34 = w34 * s23;
-                v = ((p12[0] + p12[1]) + p34[0]) + p34[1];
-            }
-            v = in ? v : 0.f;
-#else
             float v = 0.f;
             if (in) {
                 // mdmcn_im2col_bilinear (.cuh:24-54), in the window: (float)h_low == fh, so
-                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36); the (h, w)
-                // pairs and the weight / sample products in packed f32 (per-lane IEEE)
+                // h_im - fh is the reference's h_im - (float)h_low (.cuh:35-36).  Scalar f32:
+                // the same sequence as v_pk_fma / v_pk_mul pairs measured 2 % slower at C5
+                // (profiles/r03/ab_step_packed_vs_scalar_v1.txt; packed f32 issues at more
+                // than two scalar slots on gfx950), so this file is built without SLP packing
                 const float fh = floorf(h_im), fw = floorf(w_im);
-                const f32x2 l = hw2 - (f32x2){fh, fw};        // (lh, lw)
+                const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
                 const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
                 const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
-                // (hh, lh) and (hw, lw) as fma(l, (-1, 1), (1, 0)): 1 - l and l, one rounding each
-                const f32x2 hv = pk_fma_bcast<0>(l, negone, onezero);  // (hh, lh)
-                const f32x2 wv = pk_fma_bcast<1>(l, negone, onezero);  // (hw, lw)
-                const f32x2 w12 = pk_mul_bcast<0>(wv, hv), w34 = pk_mul_bcast<1>(wv, hv);  // (w1, w2), (w3, w4)
-                const f32x2 s01 = {s[0], s[1]}, s23 = {s[WW], s[WW + 1]};
-                const f32x2 p12 = w12 * s01, p34 = w34 * s23;
-                v = ((p12[0] + p12[1]) + p34[0]) + p34[1];
+                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
             }
-#endif
             col[k][p] = MIX ? __builtin_fmaf(v, (float)ak[p], 0.f) : v * (float)ak[p];  // .cuh:189 col = val * mask
         }
     }
@@ -522,8 +481,8 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
                     continue;
                 }
                 {  // served by pass A (the same test on the same values)
-                    const u32x2 rb = __builtin_bit_cast(u32x2, (f32x2){h_im, w_im} - lo2);
-                    if (rb[0] < kLimH && rb[1] < kLimW) continue;
+                    if (__builtin_bit_cast(unsigned, h_im - lo_h) < kLimH && __builtin_bit_cast(unsigned, w_im - lo_w) < kLimW)
+                        continue;
                 }
                 // invalid (.cuh:180, NaN included): the reference's val = 0, already col = 0 * a above
                 if (!(h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf)) continue;

@@ -10,3 +10,4 @@ for CFG in nyu_k16; do
   AB_CONFIG=$CFG bash scripts/gpu_ab.sh cur=- bfree=$L/libnlspn_bfree.so bfree7=$L/libnlspn_bfree7.so > $O/ab_$CFG.txt 2>&1 || { cat $O/ab_$CFG.txt; exit 1; }
   echo "== $CFG"; cat $O/ab_$CFG.txt
 done
+cd /tmp && timeout -k 10 120 rocprofv3 --list-avail > $GRAFT_REPO_ROOT/gpurun_out/r3j_$1/avail.txt 2>&1 || true

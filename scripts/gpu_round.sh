@@ -39,3 +39,14 @@ for CFG in nyu kitti nyu_k16 nyu_b1; do
 done
 # the reference's last head layers on MIOpen (input to the head-epilogue fusion work)
 cd $R && timeout -k 10 180 python tools/head_prof.py > $O/head_prof.json 2> $O/head_prof.err || exit 1
+# request-size PMC passes (read / write bytes by request width: checks the x2 FETCH_SIZE
+# correction on this code) and the C5 step kernel's SQ counters
+bash $R/scripts/gpu_pmc_req.sh $TAG nyu kitti nyu_b1 nyu_k16 || exit 1
+bash $R/scripts/gpu_c5_pmc.sh $TAG || exit 1
+# same-box A/B against the round's base library, when present
+cd $R
+if [ -f nlspn_eccv20_amd/lib/ab/libnlspn_r3base.so ]; then
+  for CFG in nyu kitti nyu_k16 nyu_b1; do
+    AB_CONFIG=$CFG bash scripts/gpu_ab.sh cur=- base=nlspn_eccv20_amd/lib/ab/libnlspn_r3base.so > $O/ab_$CFG.txt 2>&1 || exit 1
+  done
+fi
