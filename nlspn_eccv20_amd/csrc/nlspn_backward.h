@@ -59,6 +59,9 @@ struct BwdArgs {
     long long gaff_bs, goff_bs;  // batch strides of grad_aff_raw / g_off in elements (0: contiguous)
     float *gamma_part;      // one partial dL/dgamma per workgroup (TGASS), or null
     int kind;
+    // two-pass form (SPLIT): this iteration's dL/dout plane, written for bwd_coef_kernel
+    float *go_out;          // plane of item 0; item b at go_out + b * go_bs
+    long long go_bs;
 };
 
 __device__ __forceinline__ float bld(rsrc_t r, unsigned vo, unsigned so) {
@@ -144,7 +147,12 @@ __device__ __forceinline__ float aff_norm_backward(const float (&G)[K], const fl
 // registers and read-modify-write in chunks of 8 planes.
 // DIAG: diagnostic knobs for tools/bwd_bench (0 in the library; non-zero values
 // produce wrong gradients): 1 = no window flush, 4 = no accumulator read-modify-write.
-template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET, bool FIRST, int DIAG = 0>
+// SPLIT (two-pass form, offsets): the step only produces dL/dout (written to go_out) and
+// scatters dL/df_{t-1}; the dL/daff and dL/doffset terms, which need f_{t-1} at every
+// tap, are computed for all T iterations afterwards by bwd_coef_kernel.  Without the
+// clamp's mask recomputation a SPLIT step stages no window and reads no accumulator.
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET, bool FIRST, int DIAG = 0,
+          bool SPLIT = false>
 __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
@@ -159,6 +167,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     constexpr unsigned ES = 4;
     constexpr bool HOIST = K <= 8;
     constexpr int KO = OFFSET ? 2 * K : 1;
+    static_assert(!SPLIT || OFFSET, "the two-pass form is for the offset branch");
     __shared__ __attribute__((aligned(16))) float win[NC];   // f_{t-1} over the window
     __shared__ unsigned long long gacc[NC];                 // scatter accumulator for dL/df_{t-1} (fixed point)
     __shared__ float red[NT / 64], redm[NT / 64];
@@ -188,10 +197,11 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     const unsigned vpix = (active ? (unsigned)(y * W + x) : 0u) * ES, plane_bytes = (unsigned)HW * ES;
 
     // ---- 1. all loads: window staging, tap planes, own pixel, accumulators
+    const bool need_win = !SPLIT || clip;  // SPLIT: f_{t-1} only for the clamp's mask
     float sp[SIT][SV], sc[SIT][SV], sd[FIRST ? SIT : 1][SV];
     bool sin[SIT];
 #pragma unroll
-    for (int it = 0; it < SIT; ++it) {
+    for (int it = 0; it < SIT && need_win; ++it) {
         const int i = threadIdx.x + it * NT;
         const int ii = i < NV ? i : NV - 1;
         const int r = ii / WV, c = (ii - r * WV) * SV;
@@ -232,13 +242,14 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
     const rsrc_t rgo = make_rsrc(OFFSET ? a.g_off + b * (a.goff_bs ? a.goff_bs : 2LL * K * HW) : a.g_aff);
     float cG[K], cO[KO];
 #pragma unroll
-    for (int k = 0; k < K; ++k) cG[k] = (HOIST && !last && !(DIAG & 4)) ? bld(rga, vpix, gplane(k)) : 0.f;
+    for (int k = 0; k < K; ++k) cG[k] = (HOIST && !SPLIT && !last && !(DIAG & 4)) ? bld(rga, vpix, gplane(k)) : 0.f;
 #pragma unroll
-    for (int k = 0; k < KO; ++k) cO[k] = (OFFSET && HOIST && !last && !(DIAG & 4)) ? bld(rgo, vpix, (unsigned)k * plane_bytes) : 0.f;
+    for (int k = 0; k < KO; ++k)
+        cO[k] = (OFFSET && HOIST && !SPLIT && !last && !(DIAG & 4)) ? bld(rgo, vpix, (unsigned)k * plane_bytes) : 0.f;
 
     // ---- 2. stage f_{t-1}, zero the scatter window
 #pragma unroll
-    for (int it = 0; it < SIT; ++it) {
+    for (int it = 0; it < SIT && need_win; ++it) {
         const int i = threadIdx.x + it * NT;
         if (i < NV) {
             float v[SV];
@@ -279,7 +290,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             ws = (float)xx;
         }
     };
-    const float fown = win[(ly + RY) * WW + lx + RX];
+    const float fown = need_win ? win[(ly + RY) * WW + lx + RX] : 0.f;
     float asum = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) asum += av[k];
@@ -318,6 +329,7 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             if (!(pre >= 0.f)) g = 0.f;
         }
         go = preserve ? (1.0f - (dv > 0.f ? 1.f : 0.f)) * g : g;
+        if (SPLIT) bst(make_rsrc(a.go_out + b * a.go_bs), vpix, 0u, go);
         // bound on everything this pixel scatters: |go| (|a_ref| + sum |a_k|), bilinear weights <= 1
         float as = fabsf(aref);
 #pragma unroll
@@ -351,54 +363,84 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
         };
         if (exact) add_win((ly + RY) * WW + lx + RX, go * aref);  // reference tap: integer point, weight 1
         else atomicAdd(&gfw[y * W + x], go * aref);
+        if constexpr (SPLIT) {
+            // scatter only: the corner weights of every valid tap (.cuh:196-254)
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float hs, ws;
-            tap_pos(k, hs, ws);
-            float val = 0.f;
-            if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
-                int hl, wl;
-                float v[4];
-                const bool inwin = tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf,
-                                                              preserve, clip, hl, wl, v);
-                const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
-                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
-                const float top = go * av[k];
-                if (OFFSET) {
-                    float cwh = 0.f, cww = 0.f;
-                    cwh += -1 * hw * v[0];
-                    cwh += -1 * lw * v[1];
-                    cwh += hw * v[2];
-                    cwh += lw * v[3];
-                    cww += -1 * hh * v[0];
-                    cww += hh * v[1];
-                    cww += -1 * lh * v[2];
-                    cww += lh * v[3];
-                    cO[2 * k] += cwh * go * av[k];
-                    cO[2 * k + 1] += cww * go * av[k];
-                }
-                if (inwin && exact) {
-                    // out-of-image cells of the window are dropped by the flush (as the reference's checks)
-                    const int c0 = (hl - wy0) * WW + (wl - wx0);
-                    add_win(c0, w1 * top);
-                    add_win(c0 + 1, w2 * top);
-                    add_win(c0 + WW, w3 * top);
-                    add_win(c0 + WW + 1, w4 * top);
-                } else {
-                    const float wts[4] = {w1, w2, w3, w4};
+            for (int k = 0; k < K; ++k) {
+                float hs, ws;
+                tap_pos(k, hs, ws);
+                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                    const int hl = (int)floorf(hs), wl = (int)floorf(ws);
+                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    const float top = go * av[k];
+                    const bool inwin = (unsigned)(hl - wy0) < (unsigned)(WH - 1) && (unsigned)(wl - wx0) < (unsigned)(WW - 1);
+                    if (inwin && exact) {
+                        const int c0 = (hl - wy0) * WW + (wl - wx0);
+                        add_win(c0, w1 * top);
+                        add_win(c0 + 1, w2 * top);
+                        add_win(c0 + WW, w3 * top);
+                        add_win(c0 + WW + 1, w4 * top);
+                    } else {
+                        const float wts[4] = {w1, w2, w3, w4};
 #pragma unroll
-                    for (int cnr = 0; cnr < 4; ++cnr) {
-                        const int hy = hl + (cnr >> 1), wx = wl + (cnr & 1);
-                        if (hy >= 0 && hy <= H - 1 && wx >= 0 && wx <= W - 1) atomicAdd(&gfw[hy * W + wx], wts[cnr] * top);
+                        for (int cnr = 0; cnr < 4; ++cnr) {
+                            const int hy = hl + (cnr >> 1), wx = wl + (cnr & 1);
+                            if (hy >= 0 && hy <= H - 1 && wx >= 0 && wx <= W - 1) atomicAdd(&gfw[hy * W + wx], wts[cnr] * top);
+                        }
                     }
                 }
             }
-            cG[k] += go * (val - fown);
+        } else {
+    #pragma unroll
+            for (int k = 0; k < K; ++k) {
+                float hs, ws;
+                tap_pos(k, hs, ws);
+                float val = 0.f;
+                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                    int hl, wl;
+                    float v[4];
+                    const bool inwin = tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf,
+                                                                  preserve, clip, hl, wl, v);
+                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
+                    const float top = go * av[k];
+                    if (OFFSET) {
+                        float cwh = 0.f, cww = 0.f;
+                        cwh += -1 * hw * v[0];
+                        cwh += -1 * lw * v[1];
+                        cwh += hw * v[2];
+                        cwh += lw * v[3];
+                        cww += -1 * hh * v[0];
+                        cww += hh * v[1];
+                        cww += -1 * lh * v[2];
+                        cww += lh * v[3];
+                        cO[2 * k] += cwh * go * av[k];
+                        cO[2 * k + 1] += cww * go * av[k];
+                    }
+                    if (inwin && exact) {
+                        // out-of-image cells of the window are dropped by the flush (as the reference's checks)
+                        const int c0 = (hl - wy0) * WW + (wl - wx0);
+                        add_win(c0, w1 * top);
+                        add_win(c0 + 1, w2 * top);
+                        add_win(c0 + WW, w3 * top);
+                        add_win(c0 + WW + 1, w4 * top);
+                    } else {
+                        const float wts[4] = {w1, w2, w3, w4};
+    #pragma unroll
+                        for (int cnr = 0; cnr < 4; ++cnr) {
+                            const int hy = hl + (cnr >> 1), wx = wl + (cnr & 1);
+                            if (hy >= 0 && hy <= H - 1 && wx >= 0 && wx <= W - 1) atomicAdd(&gfw[hy * W + wx], wts[cnr] * top);
+                        }
+                    }
+                }
+                cG[k] += go * (val - fown);
+            }
         }
 
         // ---- accumulators
-        if (!HOIST && !last) {
+        if (!SPLIT && !HOIST && !last) {
 #pragma unroll
             for (int c0 = 0; c0 < K; c0 += 8) {
                 float t8[8];
@@ -418,11 +460,11 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
                 }
             }
         }
-        if (OFFSET && !(DIAG & 4)) {
+        if (OFFSET && !SPLIT && !(DIAG & 4)) {
 #pragma unroll
             for (int k = 0; k < KO; ++k) bst(rgo, vpix, (unsigned)k * plane_bytes, cO[k]);
         }
-        if (FIRST) {
+        if (!SPLIT && FIRST) {
             // G is final for this pixel: normalisation backward -> grad_aff_raw, dL/dgamma partial
             const rsrc_t rar = make_rsrc(a.aff_raw + b * a.aff_raw_bs);
             float ar[K], ga[K];
@@ -432,17 +474,17 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             const rsrc_t rout = make_rsrc(a.grad_aff_raw + b * (a.gaff_bs ? a.gaff_bs : (long long)K * HW));
 #pragma unroll
             for (int k = 0; k < K; ++k) bst(rout, vpix, (unsigned)k * plane_bytes, ga[k]);
-        } else if (!(DIAG & 4)) {
+        } else if (!SPLIT && !(DIAG & 4)) {
 #pragma unroll
             for (int k = 0; k < K; ++k) bst(rga, vpix, gplane(k), cG[k]);
         }
     }
-    if (FIRST && a.gamma_part) {
+    if (FIRST && !SPLIT && a.gamma_part) {
         for (int o = 32; o > 0; o >>= 1) gsum += __shfl_down(gsum, o, 64);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = gsum;
     }
     lds_barrier();
-    if (FIRST && a.gamma_part && threadIdx.x == 0) {
+    if (FIRST && !SPLIT && a.gamma_part && threadIdx.x == 0) {
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < NT / 64; ++i) s += red[i];
@@ -459,6 +501,184 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
             const int gy = wy0 + r, gx = wx0 + c;
             const long long q = (long long)gacc[i];
             if (q != 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) atomicAdd(&gfw[gy * W + gx], ldexpf((float)q, -sh));
+        }
+    }
+}
+
+// Second pass of the two-pass backward (offset branch): dL/daff and dL/doffset of all T
+// iterations, after the SPLIT steps wrote every iteration's dL/dout.  A workgroup owns
+// the same tile as the steps and loops t = T..1: it stages f_{t-1} into its LDS window,
+// reads the own pixel's dL/dout_t and adds each tap's terms to register accumulators —
+// the one-pass step's arithmetic in the same order (its accumulators start at 0 at
+// t = T and are summed t = T..1), so the results are bit-identical to it.  The affinity
+// and offset planes are read once (the one-pass form re-reads them and read-modify-
+// writes 24 accumulator planes per iteration).  Step 1's normalisation backward and
+// dL/dgamma partial run at the end.
+// dL/dout_t is stored in the gradient outputs themselves (plane t-1 of grad_off_raw's
+// 2K planes, then of grad_aff_raw's K; T <= 3K): a pixel's dL/dout values are read only
+// by its own thread, before that thread writes its gradients over them.
+struct BwdCoefArgs {
+    const float *pred_init, *pred_inter, *conf, *conf_eff, *dep, *aff, *off, *aff_raw, *gamma;
+    float *g_off, *grad_aff_raw, *gamma_part;
+    long long off_bs, aff_raw_bs, goff_bs, gaff_bs, N;  // batch strides resolved (non-zero)
+    int B, H, W, tiles_x, tiles_y, T, kind;
+    unsigned flags;
+};
+
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV>
+__global__ void __launch_bounds__(TH * TW) bwd_coef_kernel(BwdCoefArgs a) {
+    constexpr int NT = TH * TW;
+    constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
+    constexpr int PH = (KH - 1) / 2, PW = (KW - 1) / 2;
+    constexpr int WH = TH + 2 * RY, WW = TW + 2 * RX;
+    constexpr int WV = WW / SV, NV = WH * WV, SIT = (NV + NT - 1) / NT;
+    constexpr unsigned ES = 4;
+    static_assert(RY > PH && RX > PW, "window must cover the tap base grid");
+    static_assert(SV == 1 || (RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
+    __shared__ __attribute__((aligned(16))) float win[WH * WW];
+    __shared__ float red[NT / 64];
+
+    const int H = a.H, W = a.W;
+    const long long HW = (long long)H * W;
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % a.tiles_x;
+    tile /= a.tiles_x;
+    const int ty = tile % a.tiles_y;
+    const int b = tile / a.tiles_y;
+    const int x0 = tx * TW, y0 = ty * TH;
+    const int wy0 = y0 - RY, wx0 = x0 - RX;
+    const bool has_conf = a.conf != nullptr;
+    const bool preserve = (a.flags & kPreserve) != 0;
+    const bool clip = (a.flags & kAlwaysClip) != 0;
+    const int ly = threadIdx.x / TW, lx = threadIdx.x % TW;
+    const int y = y0 + ly, x = x0 + lx;
+    const bool active = (y < H) && (x < W);
+    const unsigned vpix = (active ? (unsigned)(y * W + x) : 0u) * ES, plane_bytes = (unsigned)HW * ES;
+    const float Hf = (float)H, Wf = (float)W;
+
+    const rsrc_t ra = make_rsrc(a.aff + b * (K + 1) * HW);
+    const rsrc_t ro = make_rsrc(a.off + b * a.off_bs);
+    float av[K], dh[K], dw[K], cG[K], cO[2 * K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        av[k] = bld(ra, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes);
+        dh[k] = bld(ro, vpix, (2u * k) * plane_bytes);
+        dw[k] = bld(ro, vpix, (2u * k + 1) * plane_bytes);
+        cG[k] = 0.f;
+        cO[2 * k] = cO[2 * k + 1] = 0.f;
+    }
+    const rsrc_t rgo = make_rsrc(a.g_off + b * a.goff_bs);
+    const rsrc_t rgr = make_rsrc(a.grad_aff_raw + b * a.gaff_bs);
+
+    const auto iter = [&](auto first_c, int t) {
+        constexpr bool FIRST = decltype(first_c)::value;
+        const float *pbase = FIRST ? a.pred_init + b * HW : a.pred_inter + (size_t)(t - 2) * a.N + b * HW;
+        const rsrc_t rp = make_rsrc(pbase);
+        const rsrc_t rc = make_rsrc(has_conf ? (FIRST ? a.conf : a.conf_eff) + b * HW : pbase);
+        const rsrc_t rd = make_rsrc(preserve ? a.dep + b * HW : pbase);
+        // stage f_{t-1} (bwd_step_kernel's staging)
+        float sp[SIT][SV], sc[SIT][SV], sd[FIRST ? SIT : 1][SV];
+        bool sin[SIT];
+#pragma unroll
+        for (int it = 0; it < SIT; ++it) {
+            const int i = threadIdx.x + it * NT;
+            const int ii = i < NV ? i : NV - 1;
+            const int r = ii / WV, c = (ii - r * WV) * SV;
+            int gy = wy0 + r, gx = wx0 + c;
+            sin[it] = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
+            gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
+            const unsigned q = (unsigned)(gy * W + gx) * ES;
+            BVec<float, SV>::load(rp, q, 0u, sp[it]);
+            if (has_conf) BVec<float, SV>::load(rc, q, 0u, sc[it]);
+            if (FIRST && preserve) BVec<float, SV>::load(rd, q, 0u, sd[FIRST ? it : 0]);
+        }
+        // this iteration's dL/dout at the own pixel (plane t-1 of the dL/dout store)
+        const int j = t - 1;
+        const float go = active ? (j < 2 * K ? bld(rgo, vpix, (unsigned)j * plane_bytes)
+                                             : bld(rgr, vpix, (unsigned)(j - 2 * K) * plane_bytes))
+                                : 0.f;
+#pragma unroll
+        for (int it = 0; it < SIT; ++it) {
+            const int i = threadIdx.x + it * NT;
+            if (i < NV) {
+                float v[SV];
+#pragma unroll
+                for (int e = 0; e < SV; ++e) {
+                    const float f = make_f<FIRST>(sp[it][e], has_conf ? sc[it][e] : 1.f,
+                                                  FIRST && preserve ? sd[FIRST ? it : 0][e] : 0.f, has_conf, preserve, clip);
+                    v[e] = sin[it] ? f : 0.f;
+                }
+                const int r = i / WV, c = (i - r * WV) * SV;
+                if constexpr (SV == 4)
+                    *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
+                else
+                    win[r * WW + c] = v[0];
+            }
+        }
+        lds_barrier();
+        // the taps' geometry is t-invariant: opaque moves keep the compiler from hoisting
+        // every tap's weights and addresses out of the t loop (187 VGPRs, 2 waves per SIMD)
+#pragma unroll
+        for (int k = 0; k < K; ++k) asm volatile("" : "+v"(dh[k]), "+v"(dw[k]));
+        if (active) {
+            const float fown = win[(ly + RY) * WW + lx + RX];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int tt = k < REF ? k : k + 1;
+                const int i = tt / KW, jj = tt % KW;
+                const float hs = (float)(y - PH + i) + dh[k];
+                const float ws = (float)(x - PW + jj) + dw[k];
+                float val = 0.f;
+                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                    int hl, wl;
+                    float v[4];
+                    tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf, preserve, clip, hl, wl, v);
+                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
+                    float cwh = 0.f, cww = 0.f;
+                    cwh += -1 * hw * v[0];
+                    cwh += -1 * lw * v[1];
+                    cwh += hw * v[2];
+                    cwh += lw * v[3];
+                    cww += -1 * hh * v[0];
+                    cww += hh * v[1];
+                    cww += -1 * lh * v[2];
+                    cww += lh * v[3];
+                    cO[2 * k] += cwh * go * av[k];
+                    cO[2 * k + 1] += cww * go * av[k];
+                }
+                cG[k] += go * (val - fown);
+            }
+        }
+        __syncthreads();  // the window is restaged by the next iteration
+    };
+#pragma unroll 1
+    for (int t = a.T; t >= 2; --t) iter(std::false_type{}, t);
+    iter(std::true_type{}, 1);
+
+    float gsum = 0.f;
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < 2 * K; ++k) bst(rgo, vpix, (unsigned)k * plane_bytes, cO[k]);
+        const rsrc_t rar = make_rsrc(a.aff_raw + b * a.aff_raw_bs);
+        float ar[K], ga[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) ar[k] = bld(rar, vpix, (unsigned)k * plane_bytes);
+        gsum = aff_norm_backward<K>(cG, ar, *a.gamma, a.kind, ga);
+#pragma unroll
+        for (int k = 0; k < K; ++k) bst(rgr, vpix, (unsigned)k * plane_bytes, ga[k]);
+    }
+    if (a.gamma_part) {
+        for (int o = 32; o > 0; o >>= 1) gsum += __shfl_down(gsum, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = gsum;
+        lds_barrier();
+        if (threadIdx.x == 0) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < NT / 64; ++i) s += red[i];
+            a.gamma_part[blockIdx.x] = s;
         }
     }
 }

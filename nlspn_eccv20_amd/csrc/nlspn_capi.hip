@@ -554,12 +554,12 @@ long long bwd_tiles(int B, int H, int W) {
     return (long long)B * ((H + kBwdTH - 1) / kBwdTH) * ((W + kBwdTW - 1) / kBwdTW);
 }
 
-template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET>
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool OFFSET, bool SPLIT = false>
 BwdLaunch make_bwd(BwdArgs &a, bool first) {
     static_assert(TH == kBwdTH && TW == kBwdTW, "bwd_tiles() sizes the dL/dgamma partials");
     BwdLaunch L;
-    L.fn = first ? reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, true>)
-                 : reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, false>);
+    L.fn = first ? reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, true, 0, SPLIT>)
+                 : reinterpret_cast<const void *>(&bwd_step_kernel<KH, KW, TH, TW, RY, RX, SV, OFFSET, false, 0, SPLIT>);
     a.tiles_x = (a.W + TW - 1) / TW;
     a.tiles_y = (a.H + TH - 1) / TH;
     L.grid = dim3((unsigned)(a.B * a.tiles_x * a.tiles_y));
@@ -567,7 +567,11 @@ BwdLaunch make_bwd(BwdArgs &a, bool first) {
     return L;
 }
 
-int select_bwd(BwdArgs &a, int kh, int kw, bool offset, bool vec, bool first, BwdLaunch &L) {
+int select_bwd(BwdArgs &a, int kh, int kw, bool offset, bool vec, bool first, BwdLaunch &L, bool split = false) {
+    if (split) {  // two-pass form: 3x3 with offsets only (bwd_split_ok)
+        L = vec ? make_bwd<3, 3, 8, 32, 8, 8, 4, true, true>(a, first) : make_bwd<3, 3, 8, 32, 8, 8, 1, true, true>(a, first);
+        return NLSPN_OK;
+    }
     if (!offset) {
         if (kh != 3 || kw != 3)
             return fail(NLSPN_EUNSUPPORTED, "no-offset propagation is 3x3 replicate (nlspnmodel.py:209-224)");
@@ -1169,6 +1173,14 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     const bool vec = (W % 4 == 0) && aligned(pred_init, 16) && aligned(pred_inter, 16) && aligned(conf, 16) &&
                      aligned(conf_eff, 16) && aligned(dep, 16);
     const float *pi = static_cast<const float *>(pred_inter);
+    // Two-pass form (3x3 with offsets, T <= 3K): the steps write dL/dout into the gradient
+    // outputs' planes and bwd_coef_kernel computes dL/daff, dL/doffset afterwards (see
+    // nlspn_backward.h).  NLSPN_BWD_ONEPASS=1 keeps the one-pass form (A/B only).
+    const char *onepass_env = getenv("NLSPN_BWD_ONEPASS");
+    const bool onepass = onepass_env && onepass_env[0] == '1';
+    const bool split = !onepass && off_raw && kh == 3 && kw == 3 && T <= 3 * K;
+    const long long goff_bs = grad_off_bstride ? grad_off_bstride : 2LL * K * HW;
+    const long long gaff_bs = grad_aff_bstride ? grad_aff_bstride : (long long)K * HW;
     int rc = NLSPN_OK;
     for (int t = T; t >= 1; --t) {
         const bool first = t == 1;
@@ -1201,11 +1213,48 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
             a.gamma_part = (grad_gamma && kind == NLSPN_AFF_TGASS) ? gpart : nullptr;
             a.kind = kind;
         }
+        if (split) {
+            const int j = t - 1;  // dL/dout_t -> plane j of grad_off_raw (2K planes), then of grad_aff_raw
+            a.go_out = j < 2 * K ? static_cast<float *>(grad_off_raw) + (size_t)j * HW
+                                 : static_cast<float *>(grad_aff_raw) + (size_t)(j - 2 * K) * HW;
+            a.go_bs = j < 2 * K ? goff_bs : gaff_bs;
+        }
         BwdLaunch L;
-        if ((rc = select_bwd(a, kh, kw, off_raw != nullptr, vec, first, L))) return rc;
+        if ((rc = select_bwd(a, kh, kw, off_raw != nullptr, vec, first, L, split))) return rc;
         void *args[] = {&a};
         NLSPN_HIP_TRY(hipLaunchKernel(L.fn, L.grid, L.block, args, 0, s));
         if ((rc = check_launch("nlspn_propagate_backward step"))) return rc;
+    }
+    if (split) {
+        BwdCoefArgs c{};
+        c.pred_init = static_cast<const float *>(pred_init);
+        c.pred_inter = pi;
+        c.conf = static_cast<const float *>(conf);
+        c.conf_eff = static_cast<const float *>(conf_eff);
+        c.dep = static_cast<const float *>(dep);
+        c.aff = static_cast<const float *>(aff_norm);
+        c.off = static_cast<const float *>(off_raw);
+        c.aff_raw = static_cast<const float *>(aff_raw);
+        c.gamma = gamma;
+        c.g_off = static_cast<float *>(grad_off_raw);
+        c.grad_aff_raw = static_cast<float *>(grad_aff_raw);
+        c.gamma_part = (grad_gamma && kind == NLSPN_AFF_TGASS) ? gpart : nullptr;
+        c.off_bs = off_bstride;
+        c.aff_raw_bs = aff_bstride;
+        c.goff_bs = goff_bs;
+        c.gaff_bs = gaff_bs;
+        c.N = N;
+        c.B = B; c.H = H; c.W = W;
+        c.tiles_x = (W + kBwdTW - 1) / kBwdTW;
+        c.tiles_y = (H + kBwdTH - 1) / kBwdTH;
+        c.T = T;
+        c.kind = kind;
+        c.flags = flags;
+        const void *fn = vec ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4>)
+                             : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1>);
+        void *cargs[] = {&c};
+        NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)bwd_tiles(B, H, W)), dim3(kBwdTH * kBwdTW), cargs, 0, s));
+        if ((rc = check_launch("nlspn_propagate_backward coefficients"))) return rc;
     }
     const float *pinit = static_cast<const float *>(pred_init), *pdep = static_cast<const float *>(dep),
                 *pconf = static_cast<const float *>(conf), *pce = static_cast<const float *>(conf_eff), *gf0 = gf[0];

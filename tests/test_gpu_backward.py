@@ -170,3 +170,38 @@ def test_training_step_graph_capture_matches_eager():
     torch.cuda.synchronize()
     for x, y, n in zip(ref, cap, ("pred_init", "conf", "off_aff", "gamma")):
         assert rel(y.grad.cpu().numpy(), x.grad.cpu().numpy()) <= 1e-6, n
+
+
+def _grads(B, H, W, T, seed, sigma=2.0, clip=False):
+    K = 8
+    s = synth(B, H, W, K, seed=seed, density=0.05, off_sigma=sigma)
+    rng = np.random.default_rng(seed + 1)
+    wp = torch.from_numpy(rng.standard_normal((B, 1, H, W)).astype(np.float32)).to(DEV)
+    wi = torch.from_numpy(rng.standard_normal((T, B, 1, H, W)).astype(np.float32)).to(DEV)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(True)  # noqa: E731
+    off_aff, pi, cf = t(s["off_aff"]), t(s["pred_init"]), t(s["conf"])
+    g = torch.tensor([4.0], device=DEV, requires_grad=True)
+    o = propagate(pi, torch.from_numpy(s["dep"]).to(DEV), cf, off_aff[:, 2 * K:], off_aff[:, :2 * K], g, prop_time=T,
+                  always_clip=clip)
+    ((o["pred"] * wp).sum() + (o["pred_inter_tensor"] * wi).sum()).backward()
+    torch.cuda.synchronize()
+    return {"off_aff": off_aff.grad.cpu().numpy(), "pred_init": pi.grad.cpu().numpy(), "conf": cf.grad.cpu().numpy(),
+            "gamma": g.grad.cpu().numpy()}
+
+
+@pytest.mark.parametrize("T,clip,sigma", [(18, False, 2.0), (6, True, 2.0), (12, False, 8.0)])
+def test_two_pass_backward_equals_one_pass(monkeypatch, T, clip, sigma):
+    """The two-pass backward (SPLIT steps + bwd_coef_kernel, nlspn_backward.h) issues the
+    one-pass step's arithmetic for dL/daff and dL/doffset in the same order; every gradient
+    still depends on dL/df, whose global flush uses float atomics (last bits in arrival
+    order, as the reference's col2im), so the two forms agree to float rounding."""
+    two = _grads(2, 40, 64, T, seed=T, sigma=sigma, clip=clip)
+    monkeypatch.setenv("NLSPN_BWD_ONEPASS", "1")
+    one = _grads(2, 40, 64, T, seed=T, sigma=sigma, clip=clip)
+    for k in ("off_aff", "pred_init", "conf", "gamma"):
+        assert rel(two[k], one[k]) < 1e-6, (k, rel(two[k], one[k]))
+
+
+def test_backward_long_section_one_pass_fallback(oracle):
+    """T > 3K keeps the one-pass form (the two-pass form stores dL/dout in the 3K gradient planes)."""
+    run_case(oracle, B=1, H=16, W=32, T=26, seed=3)
