@@ -193,6 +193,53 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>, optional<Tensor>> propagate
     return {pred, pred_inter, aff_out, off_out, conf_out};
 }
 
+// The propagation loop from prologued inputs (nlspnmodel.py:340-381; nlspn_propagate_normalized):
+// p0 = the blended [clamped] pred_init, the blended confidence, the normalised (K+1)-tap
+// affinity and the inserted 2(K+1)-plane offsets — what the fused head epilogue writes
+// (heads.head_epilogue_prologue).  Inference only.  -> (pred, pred_inter (T,B,1,H,W))
+std::tuple<Tensor, Tensor> propagate_normalized(const Tensor &p0, const optional<Tensor> &dep,
+                                                const optional<Tensor> &confidence, const Tensor &aff,
+                                                const Tensor &offset, int64_t prop_time, int64_t kh, int64_t kw,
+                                                bool preserve_input, bool always_clip) {
+    check_cuda("p0", p0);
+    check_cuda("aff", aff);
+    check_cuda("offset", offset);
+    TORCH_CHECK(kh % 2 == 1 && kw % 2 == 1, "only odd kernel is supported but k_f = ", kh, "x", kw);
+    TORCH_CHECK(prop_time >= 1, "prop_time must be >= 1, got ", prop_time);
+    const int64_t K = kh * kw - 1;
+    TORCH_CHECK(p0.dim() == 4 && p0.size(1) == 1, "p0 must be (B, 1, H, W)");
+    const int64_t B = p0.size(0), H = p0.size(2), W = p0.size(3);
+    for (const auto &nt : {std::make_pair("dep", &dep), std::make_pair("confidence", &confidence)})
+        if (nt.second->has_value()) check_like(nt.first, *nt.second, p0);
+    check_like("aff", aff, p0);
+    check_like("offset", offset, p0);
+    const auto exact = [&](const char *n, const Tensor &t, int64_t C) {
+        TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == C && t.size(2) == H && t.size(3) == W &&
+                        t.is_contiguous(),
+                    n, " must be a contiguous (", B, ", ", C, ", ", H, ", ", W, ") tensor, got ", t.sizes());
+    };
+    exact("p0", p0, 1);
+    if (dep.has_value()) exact("dep", *dep, 1);
+    if (confidence.has_value()) exact("confidence", *confidence, 1);
+    exact("aff", aff, K + 1);
+    exact("offset", offset, 2 * (K + 1));
+    TORCH_CHECK(!preserve_input || dep.has_value(), "preserve_input requires dep");
+    const int dt = prop_dtype(p0);
+    const auto o = p0.options();
+    Tensor pred_inter = at::empty({prop_time, B, 1, H, W}, o);
+    Tensor pred = at::empty({B, 1, H, W}, o);
+    const size_t wsb = nlspn_workspace_bytes(dt, (int)B, (int)H, (int)W);
+    Tensor ws = at::empty({(int64_t)((wsb + 3) / 4)}, o.dtype(at::kInt));
+    const unsigned flags = (preserve_input ? NLSPN_PRESERVE_INPUT : 0u) | (always_clip ? NLSPN_ALWAYS_CLIP : 0u);
+    c10::DeviceGuard guard(p0.device());
+    TORCH_CHECK(nlspn_resident_status(1) == 0, "nlspn::propagate_normalized: ", nlspn_last_error());
+    check_rc(nlspn_propagate_normalized(dt, p0.data_ptr(), ptr(dep), ptr(confidence), aff.data_ptr(), offset.data_ptr(),
+                                        pred_inter.data_ptr(), pred.data_ptr(), ws.data_ptr(), (int)B, (int)H, (int)W,
+                                        (int)kh, (int)kw, (int)prop_time, flags, stream_of(p0)),
+             "nlspn::propagate_normalized");
+    return {pred, pred_inter};
+}
+
 int dcn_dtype(const Tensor &t, bool backward) {
     if (t.scalar_type() == at::kFloat) return NLSPN_DTYPE_F32;
     if (t.scalar_type() == at::kDouble) return NLSPN_DTYPE_F64;
@@ -297,6 +344,8 @@ TORCH_LIBRARY(nlspn, m) {
     m.def("propagate(Tensor pred_init, Tensor? dep, Tensor? confidence, Tensor aff, Tensor? offset, Tensor gamma, "
           "int prop_time=18, int kh=3, int kw=3, str affinity=\"TGASS\", bool preserve_input=True, "
           "bool always_clip=False) -> (Tensor, Tensor, Tensor, Tensor?, Tensor?)");
+    m.def("propagate_normalized(Tensor p0, Tensor? dep, Tensor? confidence, Tensor aff, Tensor offset, "
+          "int prop_time=18, int kh=3, int kw=3, bool preserve_input=True, bool always_clip=False) -> (Tensor, Tensor)");
     m.def("modulated_deform_conv_forward(Tensor input, Tensor weight, Tensor? bias, Tensor offset, Tensor mask, "
           "int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h, int pad_w, int dilation_h, "
           "int dilation_w, int group, int deformable_group, int im2col_step) -> Tensor");
@@ -319,6 +368,11 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>, optional<Tensor>> propagate
     const Tensor &, int64_t, int64_t, int64_t, const std::string &, bool, bool) {
     no_cpu();
 }
+std::tuple<Tensor, Tensor> propagate_normalized_cpu(const Tensor &, const optional<Tensor> &, const optional<Tensor> &,
+                                                    const Tensor &, const Tensor &, int64_t, int64_t, int64_t, bool,
+                                                    bool) {
+    no_cpu();
+}
 Tensor mdcn_forward_cpu(const Tensor &, const Tensor &, const optional<Tensor> &, const Tensor &, const Tensor &,
                         int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t,
                         int64_t) {
@@ -335,6 +389,7 @@ TORCH_LIBRARY_IMPL(nlspn, CPU, m) {
     m.impl("affinity_normalization", &affnorm_cpu);
     m.impl("prop_step", &prop_step_cpu);
     m.impl("propagate", &propagate_cpu);
+    m.impl("propagate_normalized", &propagate_normalized_cpu);
     m.impl("modulated_deform_conv_forward", &mdcn_forward_cpu);
     m.impl("modulated_deform_conv_backward", &mdcn_backward_cpu);
 }
@@ -343,6 +398,7 @@ TORCH_LIBRARY_IMPL(nlspn, CUDA, m) {
     m.impl("affinity_normalization", &affinity_normalization);
     m.impl("prop_step", &prop_step);
     m.impl("propagate", &propagate);
+    m.impl("propagate_normalized", &propagate_normalized);
     m.impl("modulated_deform_conv_forward", &mdcn_forward);
     m.impl("modulated_deform_conv_backward", &mdcn_backward);
 }

@@ -13,6 +13,10 @@ registered below give ``torch.compile`` the output shapes without running anythi
   torch.ops.nlspn.propagate(pred_init, dep, confidence, aff, offset, gamma, prop_time,
                             kh, kw, affinity, preserve_input, always_clip)
         -> (pred, pred_inter (T,B,1,H,W), aff, offset or None, confidence or None)   :323-381
+  torch.ops.nlspn.propagate_normalized(p0, dep, confidence, aff, offset, prop_time, kh, kw,
+                                       preserve_input, always_clip) -> (pred, pred_inter)
+        the loop from prologued inputs (normalised (K+1)-tap affinity, inserted offsets:
+        what the fused head epilogue writes), :340-381; inference only
   torch.ops.nlspn.modulated_deform_conv_forward / _backward        vision.cpp:9-10
 
 Autograd (round 3): every forward op has a backward registered
@@ -88,6 +92,11 @@ def _register_fakes() -> None:
                 e((B, 2 * (K + 1), H, W)) if offset is not None else None,
                 e((B, 1, H, W)) if confidence is not None else None)
 
+    def fake_propagate_normalized(p0, dep, confidence, aff, offset, prop_time=18, kh=3, kw=3, preserve_input=True,
+                                  always_clip=False):
+        B, _, H, W = p0.shape
+        return p0.new_empty((B, 1, H, W)), p0.new_empty((prop_time, B, 1, H, W))
+
     def fake_mdcn_fwd(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
                       dilation_h, dilation_w, group, deformable_group, im2col_step):
         B, _, H, W = input.shape
@@ -100,7 +109,8 @@ def _register_fakes() -> None:
                 torch.empty_like(bias)]
 
     for name, fn in (("affinity_normalization", fake_affnorm), ("prop_step", fake_prop_step),
-                     ("propagate", fake_propagate), ("modulated_deform_conv_forward", fake_mdcn_fwd),
+                     ("propagate", fake_propagate), ("propagate_normalized", fake_propagate_normalized),
+                     ("modulated_deform_conv_forward", fake_mdcn_fwd),
                      ("modulated_deform_conv_backward", fake_mdcn_bwd)):
         torch.library.register_fake(f"nlspn::{name}")(fn)
 

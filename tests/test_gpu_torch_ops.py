@@ -204,3 +204,21 @@ def test_mdcn_op_autograd_matches_function():
     assert torch.equal(ref, got)
     for x, y, n in zip(a, b, ("input", "offset", "mask", "weight", "bias")):
         assert torch.allclose(x.grad, y.grad, rtol=1e-5, atol=1e-5), n
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_propagate_normalized_op(dtype):
+    """torch.ops.nlspn.propagate_normalized (the loop from prologued planes) == the ctypes
+    host path, bit for bit; the prologued planes come from propagate's own output dict."""
+    from nlspn_eccv20_amd import propagate_normalized
+    pi, dep, conf, aff, off, g = _inputs(dtype=dtype)
+    full = propagate(pi, dep, conf, aff, off, g, prop_time=12)
+    m = (dep > 0).to(dtype)
+    p0 = ((1 - m) * pi + m * dep).contiguous()  # the first blend (nlspnmodel.py:341-343), no clip
+    args = (p0, dep, full["confidence"], full["aff"], full["offset"])
+    pred, inter = torch.ops.nlspn.propagate_normalized(*args, 12, 3, 3, True, False)
+    ref = propagate_normalized(*args, prop_time=12)
+    torch.cuda.synchronize()
+    assert torch.equal(pred, ref["pred"]) and torch.equal(inter, ref["pred_inter_tensor"])
+    if dtype == torch.float32:  # fp16: the fused step 1 keeps p0 in f32, this p0 is rounded to f16
+        assert torch.equal(pred, full["pred"])

@@ -9,7 +9,7 @@ from nlspn_eccv20_amd import ops
 
 pytestmark = pytest.mark.skipif(not ops.available(), reason="libnlspn_torch.so not built")
 
-OPS = ("affinity_normalization", "prop_step", "propagate", "modulated_deform_conv_forward",
+OPS = ("affinity_normalization", "prop_step", "propagate", "propagate_normalized", "modulated_deform_conv_forward",
        "modulated_deform_conv_backward")
 
 
@@ -37,6 +37,8 @@ def test_fake_shapes():
         assert off is None and conf is None
         assert torch.ops.nlspn.affinity_normalization(raw[:, 16:], g, "TGASS").shape == (2, 9, 8, 16)
         assert torch.ops.nlspn.prop_step(x, x, x, aff, off, 3, 3).shape == x.shape
+        pred, inter = torch.ops.nlspn.propagate_normalized(x, x, x, aff, off, 7)
+        assert pred.shape == (2, 1, 8, 16) and inter.shape == (7, 2, 1, 8, 16)
         inp = torch.empty(2, 4, 13, 17, **d)
         w = torch.empty(6, 2, 3, 3, **d)
         o = torch.ops.nlspn.modulated_deform_conv_forward(inp, w, None, torch.empty(2, 36, 7, 9, **d),
@@ -51,6 +53,8 @@ def test_ops_reject_cpu_tensors():
     x = torch.zeros(1, 1, 4, 4)
     with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
         torch.ops.nlspn.prop_step(x, None, None, torch.zeros(1, 9, 4, 4), None, 3, 3, False, False, False)
+    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
+        torch.ops.nlspn.propagate_normalized(x, x, x, torch.zeros(1, 9, 4, 4), torch.zeros(1, 18, 4, 4), 2)
     with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
         torch.ops.nlspn.modulated_deform_conv_forward(x, torch.ones(1, 1, 3, 3), None, torch.zeros(1, 18, 4, 4),
                                                       torch.ones(1, 9, 4, 4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 64)
