@@ -517,6 +517,9 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
 // dL/dout_t is stored in the gradient outputs themselves (plane t-1 of grad_off_raw's
 // 2K planes, then of grad_aff_raw's K; T <= 3K): a pixel's dL/dout values are read only
 // by its own thread, before that thread writes its gradients over them.
+#ifndef NLSPN_BWD_COEF_WAVES
+#define NLSPN_BWD_COEF_WAVES 1
+#endif
 struct BwdCoefArgs {
     const float *pred_init, *pred_inter, *conf, *conf_eff, *dep, *aff, *off, *aff_raw, *gamma;
     float *g_off, *grad_aff_raw, *gamma_part;
@@ -526,7 +529,7 @@ struct BwdCoefArgs {
 };
 
 template <int KH, int KW, int TH, int TW, int RY, int RX, int SV>
-__global__ void __launch_bounds__(TH * TW) bwd_coef_kernel(BwdCoefArgs a) {
+__global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel(BwdCoefArgs a) {
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
     constexpr int PH = (KH - 1) / 2, PW = (KW - 1) / 2;
