@@ -393,6 +393,11 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     // arithmetic (small integers): 4 (floor(h) - wy0) WW + 4 (floor(w) - wx0)
     const float wofs = -4.f * (float)(wy0 * WW + wx0);
     bool anyout = edge_fix;  // this lane has a tap outside the window (pass B)
+    // small K (3x3): also a wave mask per tap (SGPRs), so pass B skips, wave-uniformly, the
+    // taps no lane of the wave has outside the window (a 3x3 step's 8-cell halo leaves ~1/3
+    // of its waves with some out-of-window tap at N(0, 2^2) offsets)
+    constexpr bool TAPMASK = OFFSET && K * PX <= 8;
+    uint64_t tapout[TAPMASK ? K * PX : 1];
     const auto tap_coords = [&](int k, int p, PT dh_, PT dw_, float &h_im, float &w_im) {
         const int t = k < REF ? k : k + 1;
         const int i = t / KW, j = t % KW;
@@ -444,6 +449,7 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
             tap_coords(k, p, tdh[p], tdw[p], h_im, w_im);
             const bool in = __builtin_bit_cast(unsigned, h_im - lo_h) < kLimH && __builtin_bit_cast(unsigned, w_im - lo_w) < kLimW;
             anyout |= !in;
+            if constexpr (TAPMASK) tapout[k * PX + p] = __builtin_amdgcn_ballot_w64(!in);
             float v = 0.f;
             if (in) {
                 // mdmcn_im2col_bilinear (.cuh:24-54), in the window: (float)h_low == fh, so
@@ -468,6 +474,9 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
             const int i = t / KW, j = t % KW;
 #pragma unroll
             for (int p = 0; p < PX; ++p) {
+                if constexpr (TAPMASK) {
+                    if (!edge_fix && tapout[k * PX + p] == 0) continue;  // wave-uniform
+                }
                 const unsigned c = a.off_raw ? k : t;
                 float o1[1], a1[1];
                 BVec<T, 1>::load(ro, vpix + p * ES, (2 * c) * plane_bytes, o1);
