@@ -102,6 +102,10 @@ constexpr int kResMaxNT = 768;                  // launch bound (threads per par
 #define NLSPN_RES_SMAX 1
 #endif
 constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per round
+#ifndef NLSPN_RES_PF
+#define NLSPN_RES_PF 2
+#endif
+constexpr int kResPF = NLSPN_RES_PF;             // tap-pixel slots whose LDS gathers are in flight ahead
 constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, quad columns
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
 constexpr int kResCtl = 8;                       // LDS control words ahead of the window
@@ -279,15 +283,21 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const bool active = tid < nown;
     // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned, not fused): every
     // part publishes the XCC it runs on; if all parts of its image share one, the image's
-    // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed.
+    // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed: the word
+    // is tagged with this launch (its epoch + 1, above the 5-bit XCC field), and a reader
+    // waits for THIS launch's tag, so a second launch of a section (a partial last group,
+    // unmerged groups, trace mode) never decides from the previous launch's placement.
+    // The words are zeroed once per section (step 1), and a section's launches have
+    // distinct epochs.
     const bool l2try = (a.flags & kResL2) != 0 && !fused;
     unsigned xcc_self = 0;
+    const unsigned xtag = (a.epoch + 1u) << 5;
     if (l2try) {
         unsigned x;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
         xcc_self = (x & 0xfu) + 1u;
         if (grp == 0 && tid == 0)
-            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xcc_self, __ATOMIC_RELAXED,
+            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     const float Hf = (float)H, Wf = (float)W;
@@ -542,11 +552,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 unsigned v;
                 for (;;) {
                     v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all(v != 0u)) break;
+                    if (__all((v & ~31u) == xtag)) break;
                     if (++spins > kResSpinLimit) { fail = true; break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                same = same && __all(v == xcc_self);
+                same = same && __all(v == (xtag | xcc_self));
             }
             if (lane == 0) ctl[5] = same && !fail ? 1 : 0;
         }
@@ -691,27 +701,47 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
         if (active && !(a.dbg & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            // branch-free path: every tap from the LDS window (invalid taps read zeros)
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (k == REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
-                    const float4 ar = akl[K];
-                    const float *c = &fwin[lown];
-                    acc[0] += c[0] * ar.x; acc[1] += c[1] * ar.y; acc[2] += c[2] * ar.z; acc[3] += c[3] * ar.w;
+            // branch-free path: every tap from the LDS window (invalid taps read zeros).
+            // The 32 tap-pixel slots s = 4k + e are software-pipelined: the two footprint
+            // reads of slot s + PF (and a tap's affinity row with its first slot) are issued
+            // before slot s's arithmetic, so a wave keeps LDS reads in flight instead of
+            // waiting out each gather's latency (the compiler's own schedule waited for
+            // every slot: lgkmcnt(0) per tap-pixel, profiles/r04).  Same arithmetic, same
+            // order per pixel: bit-identical.
+            constexpr int NSL = 4 * K, PF = kResPF;
+            float2 g01[NSL], g23[NSL];
+            float4 akv[K + 1], cref;
+            auto issue = [&](const int s) {
+                const int k = s >> 2, e = s & 3;
+                if (e == 0) akv[k] = akl[k];
+                if (s == 4 * REF) {  // the reference tap's own-quad cells and weight
+                    akv[K] = akl[K];
+                    cref = *reinterpret_cast<const float4 *>(&fwin[lown]);
                 }
-                const float4 a4 = akl[k];
+                const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
+                g01[s] = *reinterpret_cast<const float2 *>(fwin + idx);
+                g23[s] = *reinterpret_cast<const float2 *>(fwin + idx + WW);
+            };
+#pragma unroll
+            for (int s = 0; s < PF; ++s) issue(s);
+#pragma unroll
+            for (int s = 0; s < NSL; ++s) {
+                if (s + PF < NSL) issue(s + PF);
+                if constexpr (kResPF > 0) __builtin_amdgcn_sched_barrier(0);
+                const int k = s >> 2, e = s & 3;
+                if (PF == 0) issue(s);
+                if (s == 4 * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
+                    const float4 ar = akv[K];
+                    acc[0] += cref.x * ar.x; acc[1] += cref.y * ar.y; acc[2] += cref.z * ar.z; acc[3] += cref.w * ar.w;
+                }
+                const float4 a4 = akv[k];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float lh = lhv[k][e], lw = lwv[k][e];  // = h - (float)h_low (.cuh:35-36)
-                    const float hh = 1.f - lh, hw = 1.f - lw;
-                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
-                    const float2 s01 = *reinterpret_cast<const float2 *>(fwin + idx),
-                                 s23 = *reinterpret_cast<const float2 *>(fwin + idx + WW);
-                    const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
-                    acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
-                }
+                const float lh = lhv[k][e], lw = lwv[k][e];  // = h - (float)h_low (.cuh:35-36)
+                const float hh = 1.f - lh, hw = 1.f - lw;
+                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                const float2 s01 = g01[s], s23 = g23[s];
+                const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
+                acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
             }
             // general path (rare; only waves holding a tap outside the window): the
             // reference's per-corner checks, from global memory where needed.  It

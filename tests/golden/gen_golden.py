@@ -36,6 +36,15 @@ Round 3 adds the offset branch (verdict r2 item 3):
     offset-branch plumbing (_off_insert -> DCN offset channels, aff as the mask,
     padding, loop, blends) runs end to end.
 
+Round 4 adds gradients (verdict r3 items 4 and 5):
+  * bwd_*:  the section's gradients by the reference's own autograd (NLSPNModel.forward
+    with grad on; ModulatedDeformConvFunction's backward calls a DCN backward stand-in,
+    grid_sample_dcn_backward = autograd of the same float64 grid_sample definition):
+    offset and no-offset branch, TGASS with the s<1 clamp region, AS, TC, ASS,
+    always_clip on/off, preserve/conf_prop off, B<=2 x 40 x 56, T=18.
+  * gru_off_*:  GRU mode with learned offsets (the reference's forced default
+    configuration), outputs and gradients incl. the GRU-side weights.
+
 Outputs: tests/golden/*.npz (float32 / float16-exact inputs, allow_pickle=False) + manifest.json.
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [--cases gru,s2d]
 """
@@ -165,6 +174,69 @@ def gen_gru(nl, save, seed):
         save(name, f"forward with use_GRU=True (ConvGRU hidden/input {hd}), no offset, T={T}, {kw}", **arrs)
 
 
+def _dcn64(x, weight, bias, off, msk, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w):
+    """The DCNv2 definition on torch.grid_sample, float64, differentiable (see grid_sample_dcn)."""
+    import torch.nn.functional as F
+    B, C, H, W = x.shape
+    Cout = weight.shape[0]
+    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    ys = (torch.arange(Ho, dtype=torch.float64) * stride_h - pad_h).view(1, Ho, 1)
+    xs = (torch.arange(Wo, dtype=torch.float64) * stride_w - pad_w).view(1, 1, Wo)
+    out = torch.zeros(B, Cout, Ho, Wo, dtype=torch.float64)
+    for i in range(kernel_h):
+        for j in range(kernel_w):
+            t = i * kernel_w + j
+            h = ys + i * dilation_h + off[:, 2 * t]
+            w = xs + j * dilation_w + off[:, 2 * t + 1]
+            grid = torch.stack((2.0 * w / (W - 1) - 1.0, 2.0 * h / (H - 1) - 1.0), dim=-1)
+            val = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+            col = val * msk[:, t:t + 1]
+            out = out + torch.einsum("oc,bchw->bohw", weight[:, :, i, j], col)
+    if bias is not None:
+        out = out + bias.view(1, Cout, 1, 1)
+    return out
+
+
+def _dcn64_bilinear(x, weight, bias, off, msk, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                    dilation_w):
+    """The same DCNv2 definition with the bilinear sample written out (floor, fractions, four
+    corners each zero outside the image, the point zero outside (-1, H) x (-1, W)), float64,
+    differentiable: torch autograd of it gives the derivative the reference's col2im_coord
+    takes — the corners at floor(h), floor(w), so at an exactly integer coordinate the forward
+    difference.  (grid_sample's normalised grid loses exact integers in the round trip
+    2w/(W-1) - 1 -> (g+1)(W-1)/2 and then differentiates the other side: float16-exact
+    offsets hit integers often enough to matter for the offset gradient.)"""
+    B, C, H, W = x.shape
+    Cout = weight.shape[0]
+    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    ys = (torch.arange(Ho, dtype=torch.float64) * stride_h - pad_h).view(1, Ho, 1)
+    xs = (torch.arange(Wo, dtype=torch.float64) * stride_w - pad_w).view(1, 1, Wo)
+    flat = x.reshape(B, C, H * W)
+    out = torch.zeros(B, Cout, Ho, Wo, dtype=torch.float64)
+    for i in range(kernel_h):
+        for j in range(kernel_w):
+            t = i * kernel_w + j
+            h = ys + i * dilation_h + off[:, 2 * t]
+            w = xs + j * dilation_w + off[:, 2 * t + 1]
+            valid = (h > -1) & (w > -1) & (h < H) & (w < W)
+            hl, wl = torch.floor(h).detach(), torch.floor(w).detach()
+            lh, lw = h - hl, w - wl
+            val = torch.zeros(B, C, Ho, Wo, dtype=torch.float64)
+            for dy, dx, wt in ((0, 0, (1 - lh) * (1 - lw)), (0, 1, (1 - lh) * lw), (1, 0, lh * (1 - lw)), (1, 1, lh * lw)):
+                cy, cx = hl + dy, wl + dx
+                inb = valid & (cy >= 0) & (cy <= H - 1) & (cx >= 0) & (cx <= W - 1)
+                ind = (cy.clamp(0, H - 1) * W + cx.clamp(0, W - 1)).long().reshape(B, 1, Ho * Wo).expand(B, C, Ho * Wo)
+                v = torch.gather(flat, 2, ind).reshape(B, C, Ho, Wo)
+                val = val + torch.where(inb.unsqueeze(1), wt.unsqueeze(1) * v, torch.zeros((), dtype=torch.float64))
+            col = val * msk[:, t:t + 1]
+            out = out + torch.einsum("oc,bchw->bohw", weight[:, :, i, j], col)
+    if bias is not None:
+        out = out + bias.view(1, Cout, 1, 1)
+    return out
+
+
 def grid_sample_dcn(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
                     dilation_h, dilation_w, group, deformable_group, im2col_step):
     """A stand-in for DCN.modulated_deform_conv_forward (the signature of vision.cpp:9),
@@ -176,29 +248,35 @@ def grid_sample_dcn(input, weight, bias, offset, mask, kernel_h, kernel_w, strid
     sum over (channel, tap) with `weight`, plus `bias`.  Computed in float64 and returned
     in the input's dtype, so it rounds once where the reference's float32 CUDA kernel
     rounds per operation (~1e-7 relative)."""
-    import torch.nn.functional as F
     assert group == 1 and deformable_group == 1, "the NLSPN call: one group, one deformable group"
-    x = input.double()
-    B, C, H, W = x.shape
-    Cout = weight.shape[0]
-    Ho = (H + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
-    Wo = (W + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
-    ys = (torch.arange(Ho, dtype=torch.float64) * stride_h - pad_h).view(1, Ho, 1)
-    xs = (torch.arange(Wo, dtype=torch.float64) * stride_w - pad_w).view(1, 1, Wo)
-    off, msk = offset.double(), mask.double()
-    out = torch.zeros(B, Cout, Ho, Wo, dtype=torch.float64)
-    for i in range(kernel_h):
-        for j in range(kernel_w):
-            t = i * kernel_w + j
-            h = ys + i * dilation_h + off[:, 2 * t]
-            w = xs + j * dilation_w + off[:, 2 * t + 1]
-            grid = torch.stack((2.0 * w / (W - 1) - 1.0, 2.0 * h / (H - 1) - 1.0), dim=-1)
-            val = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
-            col = val * msk[:, t:t + 1]
-            out += torch.einsum("oc,bchw->bohw", weight[:, :, i, j].double(), col)
-    if bias is not None:
-        out += bias.double().view(1, Cout, 1, 1)
+    with torch.no_grad():
+        out = _dcn64(input.double(), weight.double(), None if bias is None else bias.double(), offset.double(),
+                     mask.double(), kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w)
     return out.to(input.dtype)
+
+
+def grid_sample_dcn_backward(input, weight, bias, offset, mask, grad_output, kernel_h, kernel_w, stride_h, stride_w,
+                             pad_h, pad_w, dilation_h, dilation_w, group, deformable_group, im2col_step):
+    """A stand-in for DCN.modulated_deform_conv_backward (vision.cpp:10; called by
+    ModulatedDeformConvFunction.backward, modulated_deform_conv_func.py:38-56): the
+    gradients of the float64 DCNv2 definition (_dcn64_bilinear) by torch autograd — grad_input (the
+    col2im scatter, .cuh:196-254), grad_offset (col2im_coord, .cuh:256-328), grad_mask,
+    grad_weight, grad_bias — returned in the input's dtype.  The derivative takes the
+    corners at floor(h), floor(w), as col2im_coord does, and is 0 for points outside
+    (-1, H) x (-1, W) as the reference's validity test makes it."""
+    assert group == 1 and deformable_group == 1, "the NLSPN call: one group, one deformable group"
+    with torch.enable_grad():
+        leaves = [t.detach().double().requires_grad_() for t in (input, offset, mask, weight)]
+        b = None if bias is None else bias.detach().double().requires_grad_()
+        x, off, msk, w = leaves
+        out = _dcn64_bilinear(x, w, b, off, msk, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                              dilation_w)
+        wrt = leaves + ([b] if b is not None else [])
+        gs = torch.autograd.grad(out, wrt, grad_output.double(), allow_unused=True)
+    gs = [torch.zeros_like(t) if g is None else g for g, t in zip(gs, wrt)]
+    g_in, g_off, g_mask, g_w = (g.to(input.dtype) for g in gs[:4])
+    g_b = gs[4].to(input.dtype) if b is not None else torch.zeros_like(weight[:, 0, 0, 0])
+    return g_in, g_off, g_mask, g_w, g_b
 
 
 OFFSET_CASES = [  # (name, prop_kernel, offset sigma, shape (B, H, W), flags): nlspnmodel.py:204-208 via the DCN stand-in
@@ -249,6 +327,134 @@ def gen_offset(nl, save, seed):
              f"B,H,W={B},{H},{W}, T=18, pred_inter planes {list(OFFLOOP_KEEP)}, {kw}", **arrs)
 
 
+BWD_CASES = [  # (name, offset, shape (B, H, W), flags): gradients of the section by the reference's autograd
+    ("bwd_off_tgass", True, (2, 40, 56), dict(affinity="TGASS", preserve_input=True, always_clip=False, conf_prop=True)),
+    ("bwd_off_tgass_clip", True, (1, 40, 56), dict(affinity="TGASS", preserve_input=True, always_clip=True,
+                                                   conf_prop=True)),
+    ("bwd_off_as", True, (1, 32, 48), dict(affinity="AS", preserve_input=True, always_clip=False, conf_prop=True)),
+    ("bwd_off_tc_noconf_nopreserve", True, (1, 32, 48), dict(affinity="TC", preserve_input=False, always_clip=False,
+                                                              conf_prop=False)),
+    ("bwd_nooff_tgass", False, (2, 40, 56), dict(affinity="TGASS", preserve_input=True, always_clip=False,
+                                                 conf_prop=True)),
+    ("bwd_nooff_ass_clip", False, (1, 32, 48), dict(affinity="ASS", preserve_input=True, always_clip=True,
+                                                    conf_prop=True)),
+]
+BWD_T = 18
+
+
+def run_forward_grad(m, pred_init, dep, off_aff, confidence):
+    """run_forward with autograd on: the heads' outputs are leaves the caller made."""
+    B, _, H, W = dep.shape
+    z = torch.zeros(B, 1, H, W)
+    const = lambda *a, **k: z  # noqa: E731
+    for name in ("conv1_rgb", "conv1_dep", "S2D", "conv2", "conv3", "conv4", "conv5",
+                 "dec4", "dec3", "dec2", "id_dec1", "off_aff_dec1", "cf_dec1"):
+        object.__setattr__(m, name, const)
+    object.__setattr__(m, "id_dec0", lambda *a: pred_init)
+    object.__setattr__(m, "off_aff_dec0", lambda *a: off_aff)
+    object.__setattr__(m, "cf_dec0", lambda *a: confidence)
+    return m.forward({"rgb": torch.zeros(B, 3, H, W), "dep": dep})
+
+
+def _section_loss(o, g, B, H, W, T):
+    """A seeded linear functional of every output the section returns: sum wp * pred +
+    sum_t wi_t * pred_inter_t (the upstream gradients, stored with the fixture)."""
+    wp = torch.randn(B, 1, H, W, generator=g).half().float()  # float16-exact (stored as float16)
+    wi = torch.randn(T, B, 1, H, W, generator=g).half().float()
+    loss = (o["pred"] * wp).sum() + (torch.stack(o["pred_inter"], 0) * wi).sum()
+    return loss, wp, wi
+
+
+def gen_backward(nl, save, seed):
+    """Gradients of the reference's own propagation section (nlspnmodel.py:317-381) by
+    torch autograd — the in-place TGASS clamp (:194), mask_fix.detach() (:330), the clamps
+    (:361, :377), gamma (:185) — with the offset branch through ModulatedDeformConvFunction
+    (modulated_deform_conv_func.py:15-56) on the grid_sample stand-ins of DCN's forward and
+    backward.  Inputs float16-exact (fixture size), computed in float32."""
+    dcn = sys.modules["DCN"]
+    dcn.modulated_deform_conv_forward = grid_sample_dcn
+    dcn.modulated_deform_conv_backward = grid_sample_dcn_backward
+    g = torch.Generator().manual_seed(seed)
+    q = lambda t: t.half().float()  # noqa: E731
+    for name, offset, (B, H, W), kw in BWD_CASES:
+        m = make_model(nl, prop_kernel=3, prop_time=BWD_T, offset=offset, **kw)
+        K = m.num_neighbors
+        pred_init, dep, conf, _ = synth(g, B, H, W, K, density=0.05)
+        aff = torch.randn(B, K, H, W, generator=g).abs()
+        aff[:, :, : H // 4] *= 0.05  # small rows: the s < 1 clamp of ASS / TGASS (:194)
+        off = torch.randn(B, 2 * K, H, W, generator=g) * 2.0
+        pred_init, dep, conf, aff, off = q(pred_init), q(dep), q(conf), q(aff), q(off)
+        off_aff = (torch.cat([off, aff], 1) if offset else aff).requires_grad_(True)
+        pi = pred_init.clone().requires_grad_(True)
+        cf = conf.clone().requires_grad_(True) if kw["conf_prop"] else None
+        o = run_forward_grad(m, pi, dep, off_aff, cf)
+        loss, wp, wi = _section_loss(o, g, B, H, W, BWD_T)
+        loss.backward()
+        arrs = dict(pred_init=pred_init.half(), dep=dep.half(), off_aff=off_aff.detach().half(),
+                    gamma=m.aff_scale_const.detach().reshape(1), w_pred=wp.half(), w_inter=wi.half(),
+                    pred=o["pred"], g_pred_init=pi.grad, g_off_aff=off_aff.grad)
+        if kw["conf_prop"]:
+            arrs.update(conf=conf.half(), g_conf=cf.grad)
+        if m.aff_scale_const.requires_grad:
+            arrs.update(g_gamma=m.aff_scale_const.grad.reshape(1))
+        save(name, f"section gradients by the reference's autograd, offset={offset} (DCN = grid_sample stand-ins), "
+             f"prop_kernel=3, B,H,W={B},{H},{W}, T={BWD_T}, loss = sum w_pred*pred + sum_t w_inter[t]*pred_inter[t], "
+             f"{kw}", **arrs)
+
+
+GRU_OFF_CASES = [  # GRU mode with learned offsets (nlspnmodel.py:303-305 + :365-373): the forced default (config.py:225-228)
+    ("gru_off_tgass_preserve", dict(affinity="TGASS", preserve_input=True, always_clip=False, conf_prop=True)),
+]
+
+
+def gen_gru_offset(nl, save, seed):
+    """NLSPNModel.forward with use_GRU=True AND offset=True: the reference's realistic
+    configuration — the offsets fixed by the head, the affinity re-estimated by the GRU every
+    iteration — through the grid_sample DCN stand-ins; outputs and the gradients (pred_init,
+    off_aff, confidence, gamma and every GRU-side weight) by the reference's autograd."""
+    stub_torchvision()
+    dcn = sys.modules["DCN"]
+    dcn.modulated_deform_conv_forward = grid_sample_dcn
+    dcn.modulated_deform_conv_backward = grid_sample_dcn_backward
+    B, H, W, T, hd = (GRU_SHAPE[k] for k in ("B", "H", "W", "T", "hidden"))
+    q = lambda t: t.half().float()  # noqa: E731
+    for n, (name, kw) in enumerate(GRU_OFF_CASES):
+        args = types.SimpleNamespace(
+            prop_kernel=3, affinity_gamma=0.5, prop_time=T, offset=True, use_GRU=True, use_S2D=False,
+            network="resnet34", from_scratch=True, zero_init_aff=False, GRU_hidden_dim=hd, GRU_input_dim=hd,
+            lr=1e-3, max_depth=10.0, patch_height=H, patch_width=W, **kw)
+        torch.manual_seed(seed + n)
+        m = nl.NLSPNModel(args)
+        g = torch.Generator().manual_seed(seed + 100 + n)
+        pred_init, dep, conf, off_aff = synth(g, B, H, W, 8, density=0.1, offset=True)
+        pred_init, dep, conf, off_aff = q(pred_init), q(dep), q(conf), q(off_aff)
+        sd = {f"sd:{k}": v for k, v in m.state_dict().items()
+              if k.split(".")[0] in ("GRU", "encode_aff", "encode_dep", "decode_aff", "aff_scale_const")}
+        with torch.no_grad():
+            o = run_forward(m, pred_init, dep, off_aff, conf if kw["conf_prop"] else None)
+        arrs = dict(pred_init=pred_init.half(), dep=dep.half(), off_aff=off_aff.half(), pred=o["pred"],
+                    pred_inter=torch.stack(o["pred_inter"], 0), aff=o["aff"], offset=o["offset"], **sd)
+        if kw["conf_prop"]:
+            arrs.update(conf=conf.half(), confidence=o["confidence"])
+        # the same forward with autograd on, and its gradients
+        oa = off_aff.clone().requires_grad_(True)
+        pi = pred_init.clone().requires_grad_(True)
+        cf = conf.clone().requires_grad_(True) if kw["conf_prop"] else None
+        m.zero_grad()
+        o2 = run_forward_grad(m, pi, dep, oa, cf)
+        loss, wp, wi = _section_loss(o2, g, B, H, W, T)
+        loss.backward()
+        arrs.update(w_pred=wp.half(), w_inter=wi.half(), g_pred_init=pi.grad, g_off_aff=oa.grad)
+        if cf is not None:
+            arrs.update(g_conf=cf.grad)
+        for k, v in m.named_parameters():
+            if f"sd:{k}" in sd and v.grad is not None:
+                arrs[f"gsd:{k}"] = v.grad
+        save(name, f"forward with use_GRU=True and offset=True (DCN = grid_sample stand-ins; ConvGRU hidden/input "
+             f"{hd}), T={T}, {kw}; outputs, then gradients of sum w_pred*pred + sum_t w_inter[t]*pred_inter[t] "
+             f"(g_* inputs, gsd:* GRU-side weights)", **arrs)
+
+
 def gen_s2d(nl, save, seed):
     for n, (B, H, W, density) in enumerate(((2, 20, 28, 0.08), (1, 13, 17, 0.5))):
         torch.manual_seed(seed + n)
@@ -269,9 +475,11 @@ def gen_s2d(nl, save, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT_DIR)
-    ap.add_argument("--cases", default="all", help="comma list of: base, gru, s2d, offset (default all)")
+    ap.add_argument("--cases", default="all",
+                    help="comma list of: base, gru, s2d, offset, backward, gru_offset (default all)")
     a = ap.parse_args()
-    which = {"base", "gru", "s2d", "offset"} if a.cases == "all" else set(a.cases.split(","))
+    which = ({"base", "gru", "s2d", "offset", "backward", "gru_offset"} if a.cases == "all"
+             else set(a.cases.split(",")))
     nl = import_reference()
     torch.set_num_threads(1)
     mpath = os.path.join(a.out, "manifest.json")
@@ -294,6 +502,10 @@ def main():
         gen_s2d(nl, save, SEED + 2000)
     if "offset" in which:
         gen_offset(nl, save, SEED + 3000)
+    if "backward" in which:
+        gen_backward(nl, save, SEED + 4000)
+    if "gru_offset" in which:
+        gen_gru_offset(nl, save, SEED + 5000)
     if "base" not in which:
         with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)

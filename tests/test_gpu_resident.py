@@ -242,6 +242,13 @@ def test_merged_groups_and_partial_group_bit_exact(dtype):
         c = propagate(*inp, prop_time=18)
     torch.cuda.synchronize()
     assert _bits_equal(a["pred_inter_tensor"], c["pred_inter_tensor"])
+    # every hand-off write-through (no same-XCD L2 mode): the launch-tagged XCC ids of the
+    # later launches (the partial group; each unmerged group) must not change the result
+    for merge in ("1", "0"):
+        with _env("1"), _env("0", "NLSPN_RES_L2"), _env(merge, "NLSPN_RES_MERGE"):
+            d = propagate(*inp, prop_time=18)
+        torch.cuda.synchronize()
+        assert _bits_equal(a["pred_inter_tensor"], d["pred_inter_tensor"]), merge
     _lib.check_resident()
 
 

@@ -3,7 +3,7 @@ stamps s_memrealtime (100 MHz) at five points of each iteration — loop top (S0
 the wait barrier (S1), after staging (S2), before the drain (S3), after the publish
 barrier (S4) — into the `pred` buffer.  Prints per-phase medians (us) per image-group
 launch; "wait" is the hand-off latency plus the skew to the slowest neighbour part.
-usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1] [--bg IMAGES_PER_LAUNCH]"""
+usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1] [--bg IMAGES_PER_LAUNCH] [--out FILE]"""
 import ctypes
 import json
 import os
@@ -21,7 +21,7 @@ from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
 CONFIGS = {"nyu": (8, 228, 304, 500 / (228 * 304)), "kitti": (4, 240, 1216, 0.05), "nyu_b1": (1, 228, 304, 500 / (228 * 304))}
 
 
-def main(config="nyu", T=18, reps=5, bg=None):
+def main(config="nyu", T=18, reps=5, bg=None, out=None):
     B, H, W, density = CONFIGS[config]
     dev = torch.device("cuda", 0)
     s = synth(B, H, W, 8, seed=7240, off_sigma=2.0, density=density)
@@ -50,7 +50,11 @@ def main(config="nyu", T=18, reps=5, bg=None):
         o = grp * bg * HW // 2  # group k's stamps start at its own pred planes (int64 = 2 floats)
         st = allst[o: o + G * T * 5].reshape(G, T, 5).astype(np.float64) / 100.0  # us
         res[f"group{grp}"] = phases(st, G, B if ng == 1 else bg, g, T)
-    print(json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res}))
+    line = json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res})
+    if out:  # the JSON alone (the runtime's stderr lines never land in the file)
+        with open(out, "w") as f:
+            f.write(line + "\n")
+    print(line)
 
 
 def phases(st, G, B, g, T):
@@ -77,5 +81,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="nyu", choices=sorted(CONFIGS))
     ap.add_argument("--bg", type=int, default=None, help="images per resident launch (C3: 2)")
+    ap.add_argument("--out", default=None, help="write the JSON line to this file")
     a = ap.parse_args()
-    main(a.config, bg=a.bg)
+    main(a.config, bg=a.bg, out=a.out)
