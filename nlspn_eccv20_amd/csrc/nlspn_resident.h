@@ -130,6 +130,7 @@ constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: 
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 constexpr unsigned kResFirst = 0x200u;            // ResArgs::flags: iteration 1 + the prologue in this launch
 constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
+constexpr unsigned kResInner = 0x800u;            // ResArgs::flags: interior quads' taps run before the neighbour wait
 // The sync workspace: one 128-B line per word group — [0] the abort word, then per part
 // i (blockIdx) the line kResLine * (1 + i) holding its progress word and (word + 1) its
 // XCC id + 1.  No two parts share a line, so a line is only ever written from one XCD.
@@ -392,11 +393,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // the general path.  Columns are whole quads plus PADX zero columns each side.
     // The setup's barriers order LDS only (lds_barrier): global stores of the fused
     // prologue stay in flight behind them.
-    if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1 - 1; ctl[3] = 4 * c0; ctl[4] = 4 * c1 - 1; }
+    // The own rectangle plus one row and one column: the reference tap's four-corner
+    // footprint (read when the window holds a non-finite f, below).  ctl[6] / ctl[7]: the
+    // per-iteration "window holds a non-finite f" flags (by iteration parity).
+    if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1; ctl[3] = 4 * c0; ctl[4] = 4 * c1; ctl[6] = ctl[7] = 0; }
     lds_barrier();
     if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
     {
-        int mn = r0, mx = r1 - 1, cmn = 4 * c0, cmx = 4 * c1 - 1;
+        int mn = r0, mx = r1, cmn = 4 * c0, cmx = 4 * c1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
@@ -623,6 +627,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // the lane id, so no VGPR holds it across the loop (it was spilled and reloaded)
         const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int nsq_it = (a.dbg & 2u) ? 0 : (rim ? nrest : nall);
+        bool nonfin = false;  // this thread staged a non-finite f
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
             int sl[SMAX];
@@ -677,6 +682,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     if (has_conf) {
                         f.x = f.x * cv[s][0]; f.y = f.y * cv[s][1]; f.z = f.z * cv[s][2]; f.w = f.w * cv[s][3];
                     }
+                    // a non-finite cell makes the sum non-finite (a finite sum that overflows
+                    // only sends the iteration to the exact four-corner form, harmlessly)
+                    nonfin |= !__builtin_isfinite((f.x + f.y) + (f.z + f.w));
                     const int li = sl[s];
                     *reinterpret_cast<float4 *>(&fwin[li]) = f;
                     fwinB[li - 1] = f.x;
@@ -685,8 +693,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
         }
+        if (__builtin_amdgcn_ballot_w64(nonfin) != 0 && lane == 0) ctl[6 + (t & 1)] = 1;
         lds_barrier();
         if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
+        // the window holds a non-finite f (staged now, or an own quad written back after
+        // the previous iteration): the reference tap takes the four-corner form below
+        const bool refull = __builtin_amdgcn_readfirstlane(ctl[6 + (t & 1)]) != 0;
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
         // The tap geometry depends only on the (invariant) coordinates, so the
@@ -710,14 +722,27 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // order per pixel: bit-identical.
             constexpr int NSL = 4 * K, PF = kResPF;
             float2 g01[NSL], g23[NSL];
-            float4 akv[K + 1], cref;
+            float4 akv[K + 1];
+            // the reference tap's samples: bilinear weights exactly (1, 0, 0, 0), so the own
+            // cell — unless the window holds a non-finite f: then the reference's four-corner
+            // sum (.cuh:37-52; 0 * inf = NaN from a right / lower neighbour; the window's zero
+            // cells outside the image are its bounds checks), a uniform branch ahead of the
+            // pipelined loop
+            float vr[4];
+            {
+                const float4 c4 = *reinterpret_cast<const float4 *>(&fwin[lown]);
+                vr[0] = c4.x; vr[1] = c4.y; vr[2] = c4.z; vr[3] = c4.w;
+                if (refull) {
+                    const float *r0p = &fwin[lown], *r1p = r0p + WW;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        vr[q] = ((1.f * r0p[q] + 0.f * r0p[q + 1]) + 0.f * r1p[q]) + 0.f * r1p[q + 1];
+                }
+            }
             auto issue = [&](const int s) {
                 const int k = s >> 2, e = s & 3;
                 if (e == 0) akv[k] = akl[k];
-                if (s == 4 * REF) {  // the reference tap's own-quad cells and weight
-                    akv[K] = akl[K];
-                    cref = *reinterpret_cast<const float4 *>(&fwin[lown]);
-                }
+                if (s == 4 * REF) akv[K] = akl[K];  // the reference tap's weight
                 const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
                 g01[s] = *reinterpret_cast<const float2 *>(fwin + idx);
                 g23[s] = *reinterpret_cast<const float2 *>(fwin + idx + WW);
@@ -732,7 +757,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if (PF == 0) issue(s);
                 if (s == 4 * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
                     const float4 ar = akv[K];
-                    acc[0] += cref.x * ar.x; acc[1] += cref.y * ar.y; acc[2] += cref.z * ar.z; acc[3] += cref.w * ar.w;
+                    acc[0] += vr[0] * ar.x; acc[1] += vr[1] * ar.y; acc[2] += vr[2] * ar.z; acc[3] += vr[3] * ar.w;
                 }
                 const float4 a4 = akv[k];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -760,7 +785,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                         if (k == REF) {
                             const float4 ar = akl[K];
                             const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
-                            s += fwin[lown + e] * arv[e];
+                            const float *r0p = &fwin[lown + e], *r1p = r0p + WW;
+                            const float vr = refull ? ((1.f * r0p[0] + 0.f * r0p[1]) + 0.f * r1p[0]) + 0.f * r1p[1] : r0p[0];
+                            s += vr * arv[e];
                         }
                         const float4 a4 = akl[k];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -842,6 +869,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         __syncthreads();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0) {
+            ctl[6 + (t & 1)] = 0;  // every tap of iteration t is done (the barrier above)
             gu32 *pw = &sync[kResLine * (1 + blockIdx.x)];
             if (l2)  // same-XCD consumers only: a plain store, the line stays in the XCD's L2
                 __hip_atomic_store(pw, epoch + (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -876,6 +904,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             fwinB[lown - 1] = f.x;
             *reinterpret_cast<float2 *>(&fwinB[lown]) = make_float2(f.y, f.z);
             fwinB[lown + 2] = f.w;
+            if (!__builtin_isfinite((f.x + f.y) + (f.z + f.w)))
+                ctl[6 + ((t + 1) & 1)] = 1;  // (benign race: every writer stores 1)
         }
     }
     }  // image groups

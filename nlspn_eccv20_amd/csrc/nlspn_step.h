@@ -259,13 +259,18 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     if (FIRST && has_conf) BVec<T, PX>::load(rc, vpix, 0u, cv);
 
     // ---- 3. finish staging into LDS (waits for the staging loads only)
-    // Edge tiles (window above or left of the image) note whether the window holds a
-    // non-finite f: only then can an invalid tap at exactly h == -1 / w == -1 (0 * f over
-    // the in-image row / column) differ from the reference's val = 0 (pass B below).
+    // Every tile notes whether its window holds a non-finite f.  Only then can
+    //  * an invalid tap at exactly h == -1 / w == -1 (0 * f over the in-image row /
+    //    column; edge tiles) differ from the reference's val = 0 (pass B below), and
+    //  * the reference tap differ from its one-cell read: the reference samples all four
+    //    corners of the integer point with weights (1, 0, 0, 0) (.cuh:37-52), so a
+    //    non-finite right / lower neighbour makes it NaN (0 * inf) — the four-corner form
+    //    below (offset branch only: the no-offset branch multiplies its centre cell,
+    //    nlspnmodel.py:215-222).
     const bool edge_tile = wy0 < 0 || wx0 < 0;
     bool nonfin = false;
     const auto stage_store = [&](int it, const float (&v)[SV]) {
-        if (edge_tile) {
+        if constexpr (OFFSET) {
 #pragma unroll
             for (int e = 0; e < SV; ++e) nonfin |= !__builtin_isfinite(v[e]);
         }
@@ -311,17 +316,16 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
             stage_store(it, v);
         }
     }
-    if (edge_tile) {
+    {
         const bool wnf = __builtin_amdgcn_ballot_w64(nonfin) != 0;
         if ((threadIdx.x & 63) == 0) win[WH * WW + threadIdx.x / 64] = wnf ? 1.f : 0.f;
     }
     lds_barrier();
     if (!active) return;  // no barrier below
-    bool edge_fix = false;  // tile-uniform
-    if (edge_tile) {
+    bool win_nf = false;  // tile-uniform: the window holds a non-finite f
 #pragma unroll
-        for (int w = 0; w < NW; ++w) edge_fix |= win[WH * WW + w] != 0.f;
-    }
+    for (int w = 0; w < NW; ++w) win_nf |= win[WH * WW + w] != 0.f;
+    const bool edge_fix = edge_tile && win_nf;
 
     // ---- FIRST: the prologue's per-pixel outputs (normalised affinity, conf', offsets)
     float fref_a[PX];  // FIRST: reference-tap weight from the normalisation (== 1 - sum, same order)
@@ -518,9 +522,13 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     float acc[PX];
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
-        // reference tap: zero offset, integer sample point -> bilinear weight exactly (1,0,0,0)
+        // reference tap: zero offset, integer sample point -> bilinear weights exactly
+        // (1, 0, 0, 0): its own cell, unless the window holds a non-finite f — then the
+        // reference's four-corner sum (.cuh:52; zero-padded window = its bounds checks)
         const float aref = FIRST ? fref_a[p] : 1.0f - asum[p];
-        const float cref = win[(ly + RY) * WW + lx + p + RX] * aref;
+        const float *sr = &win[(ly + RY) * WW + lx + p + RX];
+        const float vref = OFFSET && win_nf ? ((1.f * sr[0] + 0.f * sr[1]) + 0.f * sr[WW]) + 0.f * sr[WW + 1] : sr[0];
+        const float cref = vref * aref;
         acc[p] = 0.f;
 #pragma unroll
         for (int t = 0; t < KK; ++t) acc[p] += t == REF ? cref : col[t < REF ? t : t - 1][p];

@@ -156,6 +156,40 @@ def test_resident_nonfinite_offsets():
     assert torch.equal(a["pred_inter_tensor"].nan_to_num(7.0), b["pred_inter_tensor"].nan_to_num(7.0))
 
 
+@pytest.mark.parametrize("cell", [(30, 50), (0, 127), (63, 0), (31, 72)])
+def test_resident_reference_tap_nonfinite_neighbour(oracle, cell):
+    """An inf depth makes its LEFT and UPPER neighbours NaN through their zero-offset
+    reference tap: the reference samples all four corners of the integer point with
+    weights (1, 0, 0, 0) (modulated_deform_im2col_cuda.cuh:37-52), 0 * inf = NaN.  The
+    resident kernel (iterations 2..T) and the step launches both take the four-corner
+    form when the window holds a non-finite f: the same NaN pattern as the oracle, and
+    bit-equal values elsewhere.  Cells: interior, image corners / edges, a part seam."""
+    inp, s = _inputs(2, 64, 128, seed=21)
+    y, x = cell
+    pi, dep = inp[0].clone(), inp[1].clone()
+    pi[1, 0, y, x] = float("inf")
+    dep[1, 0, max(y - 1, 0):y + 2, max(x - 1, 0):x + 2] = 0.0  # no preserve blend over the probe
+    inp = (pi, dep) + inp[2:]
+    T = 3
+    a, b = _both(inp, T=T)
+    for k in ("pred_inter_tensor", "pred"):
+        na, nb = torch.isnan(a[k]), torch.isnan(b[k])
+        assert torch.equal(na, nb), k
+        assert torch.equal(a[k].nan_to_num(7.0, 8.0, 9.0), b[k].nan_to_num(7.0, 8.0, 9.0)), k
+    pin, dp = s["pred_init"].copy(), s["dep"].copy()
+    pin[1, 0, y, x] = np.inf
+    dp[1, 0, max(y - 1, 0):y + 2, max(x - 1, 0):x + 2] = 0.0
+    e = oracle.propagate(pin, dp, s["conf"], s["off_aff"][:, 16:], s["off_aff"][:, :16], 4.0, prop_time=T)
+    got = a["pred_inter_tensor"].cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(e["pred_inter"]))
+    # iteration 1 (step 1): the inf cell's left / upper neighbours are NaN (their own taps
+    # may hit it too; the reference tap alone guarantees it)
+    for ny, nx in ((y, x - 1), (y - 1, x), (y - 1, x - 1)):
+        if ny >= 0 and nx >= 0:
+            assert np.isnan(got[0, 1, 0, ny, nx]), (ny, nx)
+    assert np.isnan(got[1]).sum() > np.isnan(got[0]).sum()  # spreads in the resident iterations
+
+
 def test_resident_replays_stable_and_no_abort():
     """A hand-off that could read a stale plane shows up as a replay that differs."""
     inp, _ = _inputs(8, 228, 304, sigma=3.0, seed=11)
