@@ -442,10 +442,6 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const char *l2env = getenv("NLSPN_RES_L2");
     const bool l2ok = !(l2env && l2env[0] == '0') && !F && ((long long)HW * (long long)es) % 128 == 0 &&
                       aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
-    // Interior quads' taps before the neighbour wait (kResInner, nlspn_resident.h);
-    // NLSPN_RES_INNER=0 (A/B) runs every quad's taps after the staging
-    const char *ienv = getenv("NLSPN_RES_INNER");
-    const unsigned inner = (ienv && ienv[0] == '0') ? 0u : kResInner;
     for (int k = 0; k < ng; ++k) {
         const long long b0 = (long long)k * S.Bg;
         const int Bk = (int)std::min<long long>(S.Bg, B - b0);
@@ -459,7 +455,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          const_cast<void *>(at(pred_inter, b0 * HW)), const_cast<void *>(at(pred, b0 * HW)),
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
                          Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)),
-                         flags | (l2ok ? kResL2 : 0u) | inner, dbg};
+                         flags | (l2ok ? kResL2 : 0u), dbg};
         if (F) {
             ResArgs &r = P.a[k];
             r.flags |= kResFirst;

@@ -103,9 +103,15 @@ constexpr int kResMaxNT = 768;                  // launch bound (threads per par
 #endif
 constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per round
 #ifndef NLSPN_RES_PF
-#define NLSPN_RES_PF 2
+#define NLSPN_RES_PF 0
 #endif
-constexpr int kResPF = NLSPN_RES_PF;             // tap-pixel slots whose LDS gathers are in flight ahead
+// tap-pixel slots whose LDS gathers are issued ahead of their arithmetic (A/B builds; 1-4
+// measured 3-5 % slower at C2 than the compiler's own schedule: the taps are bound by the
+// LDS array's bank-conflict cycles, not its latency, profiles/r04/ab_pf_r4b.txt)
+constexpr int kResPF = NLSPN_RES_PF;
+#ifndef NLSPN_RES_EXP
+#define NLSPN_RES_EXP 0  // timing experiments only (tools/res_trace.py): 1 no gathers, 2 no tap arithmetic
+#endif
 constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, quad columns
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
 constexpr int kResCtl = 8;                       // LDS control words ahead of the window
@@ -130,7 +136,6 @@ constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: 
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 constexpr unsigned kResFirst = 0x200u;            // ResArgs::flags: iteration 1 + the prologue in this launch
 constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
-constexpr unsigned kResInner = 0x800u;            // ResArgs::flags: interior quads' taps run before the neighbour wait
 // The sync workspace: one 128-B line per word group — [0] the abort word, then per part
 // i (blockIdx) the line kResLine * (1 + i) holding its progress word and (word + 1) its
 // XCC id + 1.  No two parts share a line, so a line is only ever written from one XCD.
@@ -424,7 +429,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     lds_barrier();
     int rlo = ctl[1], rhi = ctl[2], wq0 = ctl[3] >> 2, wq1 = ctl[4] >> 2;  // >> 2: floor for negatives too
     if (rhi < rlo + 1) rhi = rlo + 1;  // at least two rows (the zero redirect reads a 2x2 footprint)
-    if ((rhi - rlo + 1) * (4 * (wq1 - wq0 + 1) + 2 * PADX) > WC) {  // too large: fixed halo + general path
+    // the dynamic window holds every valid tap's footprint by construction (workgroup-uniform)
+    const bool dynwin = (rhi - rlo + 1) * (4 * (wq1 - wq0 + 1) + 2 * PADX) <= WC;
+    if (!dynwin) {  // too large: fixed halo + general path
         rlo = r0 - RY;
         rhi = r1 - 1 + RY;
         wq0 = c0 - RXQ;
@@ -447,8 +454,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     //  * in the LDS window: the branch-free path;
     //  * valid but outside the window (only with the fixed halo): read from global
     //    memory by the general path (has_fb); the dependency rectangle covers it.
+    // With the dynamic window no valid tap is outside it, so only the redirect of invalid
+    // taps runs then (the whole pass took 4.2 us of the C2 setup, profiles/r04).
     bool has_fb = false;
-    {
+    if (!dynwin) {
         int mn = H, mx = -1, cmn = W, cmx = -1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -473,8 +482,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         has_fb = has_fb && active;
         res_span_merge(ctl, has_fb, mn, mx, cmn, cmx);
+        lds_barrier();
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!(hy[k][e] > -1.f && hx[k][e] > -1.f && hy[k][e] < Hf && hx[k][e] < Wf)) {  // invalid
+                    hy[k][e] = (float)rlo;
+                    hx[k][e] = (float)(4 * wq0 - PADX);
+                }
+            }
+        }
     }
-    lds_barrier();
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
     // the parts this one reads: a rectangle of the image's part grid
     const int dy0 = res_owner(ctl[1], H, a.gy), dy1 = res_owner(ctl[2], H, a.gy);
@@ -713,39 +733,32 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
         if (active && !(a.dbg & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            // branch-free path: every tap from the LDS window (invalid taps read zeros).
-            // The 32 tap-pixel slots s = 4k + e are software-pipelined: the two footprint
-            // reads of slot s + PF (and a tap's affinity row with its first slot) are issued
-            // before slot s's arithmetic, so a wave keeps LDS reads in flight instead of
-            // waiting out each gather's latency (the compiler's own schedule waited for
-            // every slot: lgkmcnt(0) per tap-pixel, profiles/r04).  Same arithmetic, same
-            // order per pixel: bit-identical.
+            // branch-free path: every tap from the LDS window (invalid taps read zeros), in
+            // 32 tap-pixel slots s = 4k + e.  kResPF > 0 (A/B builds) issues slot s + PF's two
+            // footprint reads before slot s's arithmetic; the default leaves the schedule to
+            // the compiler (waits per slot), which measured faster: nine waves per CU already
+            // keep the LDS array busy, and its bank-conflict cycles, not the read latency,
+            // bound the taps (profiles/r04).  Same arithmetic, same order per pixel either way.
             constexpr int NSL = 4 * K, PF = kResPF;
             float2 g01[NSL], g23[NSL];
             float4 akv[K + 1];
-            // the reference tap's samples: bilinear weights exactly (1, 0, 0, 0), so the own
-            // cell — unless the window holds a non-finite f: then the reference's four-corner
-            // sum (.cuh:37-52; 0 * inf = NaN from a right / lower neighbour; the window's zero
-            // cells outside the image are its bounds checks), a uniform branch ahead of the
-            // pipelined loop
-            float vr[4];
-            {
-                const float4 c4 = *reinterpret_cast<const float4 *>(&fwin[lown]);
-                vr[0] = c4.x; vr[1] = c4.y; vr[2] = c4.z; vr[3] = c4.w;
-                if (refull) {
-                    const float *r0p = &fwin[lown], *r1p = r0p + WW;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        vr[q] = ((1.f * r0p[q] + 0.f * r0p[q + 1]) + 0.f * r1p[q]) + 0.f * r1p[q + 1];
-                }
-            }
+            float4 cref;  // the reference tap's own-quad cells (one-cell form; the four-corner
+                          // form is applied after the taps, below)
             auto issue = [&](const int s) {
                 const int k = s >> 2, e = s & 3;
                 if (e == 0) akv[k] = akl[k];
-                if (s == 4 * REF) akv[K] = akl[K];  // the reference tap's weight
+                if (s == 4 * REF) {  // the reference tap's own-quad cells and weight
+                    akv[K] = akl[K];
+                    cref = *reinterpret_cast<const float4 *>(&fwin[lown]);
+                }
                 const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
+#if NLSPN_RES_EXP == 1  // timing experiment: no gathers (wrong results)
+                g01[s] = make_float2(__builtin_bit_cast(float, idx), 1.f);
+                g23[s] = make_float2(2.f, __builtin_bit_cast(float, idx + 1u));
+#else
                 g01[s] = *reinterpret_cast<const float2 *>(fwin + idx);
                 g23[s] = *reinterpret_cast<const float2 *>(fwin + idx + WW);
+#endif
             };
 #pragma unroll
             for (int s = 0; s < PF; ++s) issue(s);
@@ -757,7 +770,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if (PF == 0) issue(s);
                 if (s == 4 * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
                     const float4 ar = akv[K];
-                    acc[0] += vr[0] * ar.x; acc[1] += vr[1] * ar.y; acc[2] += vr[2] * ar.z; acc[3] += vr[3] * ar.w;
+                    acc[0] += cref.x * ar.x; acc[1] += cref.y * ar.y; acc[2] += cref.z * ar.z; acc[3] += cref.w * ar.w;
                 }
                 const float4 a4 = akv[k];
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -765,8 +778,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float hh = 1.f - lh, hw = 1.f - lw;
                 const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
                 const float2 s01 = g01[s], s23 = g23[s];
+#if NLSPN_RES_EXP == 2  // timing experiment: gathers only, minimal arithmetic (wrong results)
+                (void)w1; (void)w2; (void)w3; (void)w4;
+                acc[e] += (s01.x + s01.y) + (s23.x + s23.y);
+#else
                 const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                 acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
+#endif
             }
             // general path (rare; only waves holding a tap outside the window): the
             // reference's per-corner checks, from global memory where needed.  It
@@ -785,9 +803,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                         if (k == REF) {
                             const float4 ar = akl[K];
                             const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
-                            const float *r0p = &fwin[lown + e], *r1p = r0p + WW;
-                            const float vr = refull ? ((1.f * r0p[0] + 0.f * r0p[1]) + 0.f * r1p[0]) + 0.f * r1p[1] : r0p[0];
-                            s += vr * arv[e];
+                            s += fwin[lown + e] * arv[e];
                         }
                         const float4 a4 = akl[k];
                         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -840,6 +856,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     }
                     acc[e] = s;
                 }
+            }
+            // the reference tap in the reference's four-corner form (.cuh:37-52: the integer
+            // point's weights are exactly (1, 0, 0, 0)) differs from the one-cell form used
+            // above only when its right / lower neighbour is non-finite: 0 * inf = NaN, and
+            // a NaN term makes the whole tap sum NaN whatever its position (any other
+            // difference is the sign of a zero term, which an accumulator starting at +0
+            // never shows).  A uniform branch, taken only when the window holds a
+            // non-finite f; the window's zero cells outside the image are its bounds checks.
+            if (refull) {
+                const float *r0p = &fwin[lown], *r1p = r0p + WW;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (!__builtin_isfinite(r0p[e + 1]) || !__builtin_isfinite(r1p[e]) || !__builtin_isfinite(r1p[e + 1]))
+                        acc[e] = __builtin_nanf("");
             }
             float o[4], fin[4];
             const float4 d4 = akl[K + 2];

@@ -119,6 +119,13 @@ __device__ __forceinline__ float fma_mix_lo(_Float16 a, float b, float c) {
 #define NLSPN_STEP_F16_WAVES 6
 #endif
 constexpr int kStepF16Waves = NLSPN_STEP_F16_WAVES;
+#ifndef NLSPN_STEP_PAIR
+#define NLSPN_STEP_PAIR 0
+#endif
+// offset branch: paired window copies (ds_read_b64); A/B builds only — C5 measured 2.5 %
+// slower with them (the second copy's staging writes and the copy select cost more than the
+// halved footprint reads save, profiles/r04/ab_r4e_nyu_k16.txt)
+constexpr bool kStepPair = NLSPN_STEP_PAIR != 0;
 
 // KH x KW taps; TH x TW tile; PX px per thread; window radii RY/RX; SV = staging
 // vector width (4 requires W % 4 == 0 and RX % 4 == 0); PRE = issue every tap's
@@ -142,8 +149,15 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     constexpr int SIT = (NV + NT - 1) / NT;      // staging vectors per thread
     constexpr unsigned ES = sizeof(T);
     constexpr int NW = NT / 64;
-    // the window, then one word per wave: "this wave staged a non-finite f" (edge tiles)
-    __shared__ __attribute__((aligned(16))) float win[WH * WW + NW];
+    // the window, then one word per wave: "this wave staged a non-finite f".  PAIR (offset
+    // branch): a second copy shifted by one cell (winB[i] = win[i + 1], from WP on), so any
+    // horizontal pair of a bilinear footprint is ONE 8-byte-aligned ds_read_b64 from one of
+    // the two copies (the resident kernel's form) instead of a ds_read2_b32 (two 32-lane
+    // passes): half the LDS instructions per footprint row.
+    constexpr bool PAIR = OFFSET && kStepPair;
+    constexpr int WP = (WH * WW + NW + 4) & ~3;  // copy B's base (16-B aligned), behind the flags
+    __shared__ __attribute__((aligned(16))) float win[PAIR ? WP + WH * WW + 4 : WH * WW + NW];
+    float *winB = win + WP;  // winB[i] = cell i + 1 (winB[-1] is padding): an odd cell's pair is 8-B aligned
 
     const int H = a.H, W = a.W;
     const long long HW = (long long)H * W;
@@ -280,6 +294,16 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
             *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
         else
             win[r * WW + c] = v[0];
+        if constexpr (PAIR) {  // copy B: cell (r, c + e) at winB[r * WW + c + e - 1]
+            const int li = r * WW + c;
+            if constexpr (SV == 4) {
+                winB[li - 1] = v[0];
+                *reinterpret_cast<float2 *>(&winB[li]) = make_float2(v[1], v[2]);  // li % 4 == 0
+                winB[li + 2] = v[3];
+            } else {
+                winB[li - 1] = v[0];
+            }
+        }
     };
     if constexpr (MIXS) {  // out-of-image cells loaded as zeros: 0 * 0 = +0
         // two loops under the uniform has_conf branch (one select per cell otherwise)
@@ -464,9 +488,18 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
                 const float fh = floorf(h_im), fw = floorf(w_im);
                 const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
                 const unsigned bo = (unsigned)__builtin_fmaf(fh, (float)(4 * WW), __builtin_fmaf(fw, 4.f, wofs));
-                const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
                 const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
+                if constexpr (PAIR) {
+                    // an odd cell's pair is in copy B, one cell lower: + 4 * (WP - 1) bytes
+                    const unsigned ba = bo + (bo & 4u) * (unsigned)(WP - 1);
+                    const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + ba);
+                    const float2 s01 = *reinterpret_cast<const float2 *>(s);
+                    const float2 s23 = *reinterpret_cast<const float2 *>(s + WW);
+                    v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
+                } else {
+                    const float *s = reinterpret_cast<const float *>(reinterpret_cast<const char *>(win) + bo);
+                    v = (w1 * s[0] + w2 * s[1] + w3 * s[WW] + w4 * s[WW + 1]);
+                }
             }
             col[k][p] = MIX ? __builtin_fmaf(v, (float)ak[p], 0.f) : v * (float)ak[p];  // .cuh:189 col = val * mask
         }

@@ -351,6 +351,10 @@ class _PropagateFn(torch.autograd.Function):
             _lib.check_resident()  # an earlier resident launch that aborted raises here
             _lib.check(_lib.get().nlspn_propagate(*args, _stream(pred_init.device)))
         ctx.cfg = (kh, kw, int(prop_time), affinity, preserve_input, always_clip)
+        # an unused output's gradient arrives as None, not as a zero-filled tensor: a loss
+        # on `pred` alone then neither fills nor reads the (T, B, 1, H, W) pred_inter
+        # gradient (the C ABI takes null grad_pred / grad_pred_inter)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(pred_init, dep, confidence, aff, offset, gamma, outs["pred_inter"], outs["aff"],
                               outs["confidence"])
         nd = [t for t in (outs["aff"], outs["offset"], outs["confidence"]) if t is not None]
