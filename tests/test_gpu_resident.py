@@ -57,9 +57,16 @@ def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=
             oa[:, 16:], oa[:, :16], torch.tensor([4.0], device=DEV)), s
 
 
-def _both(inp, T=18, **kw):
+def _nan_equal(x, y):
+    """Equal NaN positions and bit-equal values elsewhere (a NaN's payload depends on which
+    operation made it, not on the propagation it encodes)."""
+    return torch.equal(torch.isnan(x), torch.isnan(y)) and _bits_equal(x.nan_to_num(7.0), y.nan_to_num(7.0))
+
+
+def _both(inp, T=18, nan_ok=False, **kw):
     """(resident, steps): the default resident form (behind a step-1 launch), checked
-    here against the resident form with iteration 1 inside the launches, and the step form."""
+    here against the resident form with iteration 1 inside the launches, and the step form.
+    nan_ok: NaN results compare by position (_nan_equal)."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
         with _env("1", "NLSPN_RES_FIRST"):
@@ -71,8 +78,9 @@ def _both(inp, T=18, **kw):
         if a[k] is not None or b[k] is not None:
             assert _bits_equal(a[k], b[k]), k
             assert _bits_equal(c[k], b[k]), k
-    assert _bits_equal(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
-    assert _bits_equal(a["pred"], c["pred"])
+    eq = _nan_equal if nan_ok else _bits_equal
+    assert eq(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
+    assert eq(a["pred"], c["pred"])
     return a, b
 
 
@@ -171,11 +179,9 @@ def test_resident_reference_tap_nonfinite_neighbour(oracle, cell):
     dep[1, 0, max(y - 1, 0):y + 2, max(x - 1, 0):x + 2] = 0.0  # no preserve blend over the probe
     inp = (pi, dep) + inp[2:]
     T = 3
-    a, b = _both(inp, T=T)
+    a, b = _both(inp, T=T, nan_ok=True)
     for k in ("pred_inter_tensor", "pred"):
-        na, nb = torch.isnan(a[k]), torch.isnan(b[k])
-        assert torch.equal(na, nb), k
-        assert torch.equal(a[k].nan_to_num(7.0, 8.0, 9.0), b[k].nan_to_num(7.0, 8.0, 9.0)), k
+        assert _nan_equal(a[k], b[k]), k
     pin, dp = s["pred_init"].copy(), s["dep"].copy()
     pin[1, 0, y, x] = np.inf
     dp[1, 0, max(y - 1, 0):y + 2, max(x - 1, 0):x + 2] = 0.0
