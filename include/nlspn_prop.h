@@ -57,8 +57,8 @@ extern "C" {
 #define NLSPN_EUNSUPPORTED 2 /* geometry or dtype without a kernel instantiation */
 #define NLSPN_EHIP 3         /* HIP runtime / launch error */
 #define NLSPN_EABORTED 4     /* a resident launch aborted (nlspn_resident_status) */
-/* nlspn_time_propagate *resident: bit set when iteration 1 ran inside the resident
- * launches (no step-1 kernel; *first_ms is then ~0) */
+/* nlspn_time_propagate *resident: bit once set when iteration 1 ran inside the resident
+ * launches (an A/B form removed in round 4; never set now, kept for ABI stability) */
 #define NLSPN_RESIDENT_FIRST 0x100
 
 /* Version of this ABI (NLSPN_ABI_VERSION). */
@@ -162,8 +162,10 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
                     int B, int H, int W, int kh, int kw, unsigned flags, void *stream);
 
 /* Bytes of device workspace nlspn_propagate uses: the resident kernel's abort word
- * (index 0) and progress words (one 32-bit word per workgroup, from index 1).  With
- * a NULL workspace nlspn_propagate runs iterations 2..T as T-1 launches instead. */
+ * (index 0) and one 128-byte line per workgroup (its placement word).  With a NULL
+ * workspace nlspn_propagate runs iterations 2..T as T-1 launches instead.  The resident
+ * kernel also uses pred_inter itself for its hand-offs: planes 1..T-2 hold a poison
+ * value (a signalling NaN) until written, so they must not alias any input. */
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
 
 /*
@@ -178,9 +180,7 @@ size_t nlspn_workspace_bytes(int dtype, int B, int H, int W);
  *              offsets, W % 4 == 0, 16-B aligned planes, every rectangular part fits
  *              a workgroup: nlspn_resident_config), else T-1 nlspn_prop_step
  *              launches; pred_inter[t] each, the last also pred.
- *   NLSPN_RES_FIRST=1: step 1 moves into the resident launches too (their setup runs
- *   the prologue, a memset node zeroes the progress words; measured slower, kept as
- *   an A/B).  Every form is bit-identical.
+ *   Every form is bit-identical.
  * Inputs : pred_init, dep (B planes), conf (B planes, or NULL = conf_prop off),
  *          aff_raw (B x K planes, stride aff_bstride), off_raw (B x 2K planes,
  *          stride off_bstride, or NULL = no-offset branch), gamma (device f32).
@@ -230,6 +230,12 @@ int nlspn_plan_destroy(nlspn_plan_t plan);
  * dep receives no gradient (the reference's sparse input).  workspace:
  * nlspn_backward_workspace_bytes() bytes.  dL/df is scattered with float
  * atomics (as the reference's col2im), so its last bits depend on arrival order.
+ * Scratch use: the two-pass form (3x3 with offsets, T <= 3K: the default there)
+ * first stores each iteration's dL/d(output) plane in grad_aff_raw / grad_off_raw
+ * (the 3K planes per item they span together) and overwrites them with the gradients
+ * in its second pass.  So neither may overlap any input, pred_inter, aff_norm,
+ * conf_eff, the incoming gradients or each other (beyond the packed (B, 3K, H, W)
+ * layout above), and after a failed call their contents are undefined.
  */
 size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw);
 int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -333,8 +339,6 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
  * (first_ms) and of iterations 2..T (rest_ms: from the start of the first
  * resident launch to the end of the last, or the sum of the T-1 step kernels);
  * *resident = the number of resident launches (image groups), 0 for step launches,
- * | NLSPN_RESIDENT_FIRST when those launches also ran iteration 1 (rest_ms then spans
- * iterations 1..T).
  */
 int nlspn_time_propagate(int dtype, const void *pred_init, const void *dep, const void *conf,
                          const void *aff_raw, int64_t aff_bstride, const void *off_raw,

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 
 import torch  # noqa: F401  (load torch's HIP runtime before our library)
 
@@ -68,6 +69,10 @@ SIGNATURES = {
     "nlspn_affinity_normalize_backward": (_i, [_i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
 }
 
+# Entry points an A/B build (NLSPN_LIB_PATH) of an earlier round may lack; any other
+# missing symbol fails the load (a stale or wrong library is refused up front)
+AB_OPTIONAL = frozenset({"nlspn_resident_status", "nlspn_resident_config"})
+
 _lib = None
 
 
@@ -89,12 +94,16 @@ def get() -> ctypes.CDLL:
                 "`make -C nlspn_eccv20_amd/csrc` or __graft_entry__.build(). "
                 "There is no CPU fallback for the propagation hot path.")
         lib = ctypes.CDLL(LIB_PATH)
+        skipped = []
         for name, (res, args) in SIGNATURES.items():
-            if not hasattr(lib, name) and os.environ.get("NLSPN_LIB_PATH"):
-                continue  # A/B against an older build: entry points added since are absent
+            if not hasattr(lib, name) and os.environ.get("NLSPN_LIB_PATH") and name in AB_OPTIONAL:
+                skipped.append(name)  # A/B against an older build: entry points added since are absent
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if skipped:
+            warnings.warn(f"NLSPN_LIB_PATH={LIB_PATH}: entry points absent from this build: {', '.join(skipped)}")
         _lib = lib
     return _lib
 

@@ -236,6 +236,7 @@ struct DevState {
     hipStream_t last_stream = nullptr;
     bool any = false, multi = false;
     bool init = false;
+    std::vector<std::pair<const void *, int>> lds_attr;  // kernels whose LDS limit is raised (set_lds_attr)
 };
 constexpr int kMaxDevices = 64;
 DevState g_dev[kMaxDevices];
@@ -260,6 +261,24 @@ DevState *dev_state() {
         d.init = true;
     }
     return &d;
+}
+
+// Raises a kernel's dynamic-LDS limit once per (device, kernel, size): the attribute is
+// per device, and launches come from several threads and devices, so it is checked on
+// every launch, but the driver call is made only the first time.
+int set_lds_attr(const void *fn, int lds) {
+    DevState *d = dev_state();
+    if (d) {
+        std::lock_guard<std::mutex> lk(d->m);
+        for (const auto &e : d->lds_attr)
+            if (e.first == fn && e.second >= lds) return NLSPN_OK;
+    }
+    NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    if (d) {
+        std::lock_guard<std::mutex> lk(d->m);
+        d->lds_attr.emplace_back(fn, lds);
+    }
+    return NLSPN_OK;
 }
 
 bool stream_capturing(hipStream_t s) {
@@ -309,7 +328,6 @@ struct ResPlan {
     unsigned block = 0;
     size_t lds = 0, sync_bytes = 0;
     int ngroups = 0;
-    bool first = false;  // iteration 1 runs in the launches (ResFirstIn)
     unsigned grid[kResMaxGroups] = {};
     ResArgs a[kResMaxGroups];
 };
@@ -378,30 +396,16 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
     return false;
 }
 
-// Iteration 1 and the forward prologue inside the resident launches (ResArgs kResFirst):
-// the raw inputs step 1 would read; conf_eff / aff_norm of plan_resident are then the
-// conf_out / aff_out the launches write.
-struct ResFirstIn {
-    const void *pinit, *conf_raw, *aff_raw;
-    long long aff_bs;
-    void *off_out;
-    const float *gamma;
-    int kind;
-};
-
-// Fills P and returns true when the resident kernel applies (with F: iterations 1..T).
+// Fills P and returns true when the resident kernel applies (iterations 2..T).
 bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
-                   int kw, int T, unsigned flags, ResPlan &P, const ResFirstIn *F = nullptr) {
+                   int kw, int T, unsigned flags, ResPlan &P) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
     const size_t es = esize(dtype), vb = 4 * es;
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
-        return false;
-    if (F && (!aligned(F->pinit, vb) || !aligned(F->conf_raw, vb) || !aligned(F->aff_raw, vb) || F->aff_bs % 4 != 0 ||
-              !aligned(F->off_out, vb) || !F->gamma || ((flags & kPreserve) && !dep)))
         return false;
     const int cus = device_cus();
     if (cus < 1) return false;
@@ -447,7 +451,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // by two images), not with the fused prologue; NLSPN_RES_L2=0 (A/B) keeps every
     // hand-off write-through
     const char *l2env = getenv("NLSPN_RES_L2");
-    const bool l2ok = !(l2env && l2env[0] == '0') && !F && ((long long)HW * (long long)es) % 128 == 0 &&
+    const bool l2ok = !(l2env && l2env[0] == '0') && ((long long)HW * (long long)es) % 128 == 0 &&
                       aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
     for (int k = 0; k < ng; ++k) {
         const long long b0 = (long long)k * S.Bg;
@@ -463,19 +467,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
                          Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)),
                          flags | (l2ok ? kResL2 : 0u), dbg};
-        if (F) {
-            ResArgs &r = P.a[k];
-            r.flags |= kResFirst;
-            r.pinit = at(F->pinit, b0 * HW);
-            r.conf_raw = at(F->conf_raw, b0 * HW);
-            r.aff_raw = at(F->aff_raw, b0 * F->aff_bs);
-            r.aff_bs = F->aff_bs;
-            r.off_out = const_cast<void *>(at(F->off_out, b0 * 2 * (K + 1) * HW));
-            r.gamma = F->gamma;
-            r.kind = F->kind;
-        }
     }
-    P.first = F != nullptr;
     // The full image groups run in turn inside ONE launch (ResArgs::ngroups): no launch
     // boundary between them, so a part sets up its next group while others finish the
     // current one.  A partial last group keeps a launch of its own (its grid differs).
@@ -498,22 +490,13 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     return true;
 }
 
-// The progress words must be zero on entry: step 1 zeroes them (StepArgs::zero_words),
-// or (P.first: no step 1) a memset node here.
+// The sync words must be zero on entry and plane 1 poisoned (T >= 3): step 1 does both
+// (StepArgs::zero_words, ::poison).
 // e0 is recorded at the start of the first group's launch, e1 at the end of the last.
 int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
-    NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
+    if (int rc = set_lds_attr(P.fn, (int)P.lds)) return rc;
     if (P.fn_merged)
-        NLSPN_HIP_TRY(hipFuncSetAttribute(P.fn_merged, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds));
-    if (P.first) {
-        if (g_rec) {
-            LaunchRec z{};
-            z.zptr = P.a[0].sync;
-            z.zbytes = P.sync_bytes;
-            g_rec->push_back(z);
-        }
-        NLSPN_HIP_TRY(hipMemsetAsync(P.a[0].sync, 0, P.sync_bytes, s));
-    }
+        if (int rc = set_lds_attr(P.fn_merged, (int)P.lds)) return rc;
     for (int k = 0; k < P.ngroups; ++k) {
         const void *fn = k == 0 && P.fn_merged ? P.fn_merged : P.fn;
         if (g_rec)
@@ -655,28 +638,12 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
 
     if (resident) *resident = 0;
     ResPlan P;
-    // NLSPN_RES_FIRST=1: iterations 1..T resident, the prologue in the launches' setup
-    // (no step-1 launch).  Bit-identical, but not the default: measured slower (C2 144.4
-    // vs 143.4 us, C3 314 vs 307 us) — the setup, one workgroup per CU,
-    // reads the raw planes from HBM at ~2.3 TB/s, where step 1 streams them at full
-    // occupancy and the resident setup then re-reads its outputs from cache.
-    const char *fenv = getenv("NLSPN_RES_FIRST");
-    const ResFirstIn F{pred_init, conf, aff_raw, aff_bstride, off_out, gamma, kind};
-    if (fenv && fenv[0] == '1' &&
-        plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter, pred,
-                      workspace, B, H, W, kh, kw, T, flags, P, &F)) {
-        if (resident) *resident = P.ngroups | NLSPN_RESIDENT_FIRST;
-        if (ev) {  // no step-1 kernel: an empty interval
-            NLSPN_HIP_TRY(hipEventRecord(ev[0], s));
-            NLSPN_HIP_TRY(hipEventRecord(ev[1], s));
-        }
-        return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
-    }
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
                                    pred, workspace, B, H, W, kh, kw, T, flags, P);
-    if (res) {  // step 1 zeroes the resident kernel's progress words
+    if (res) {  // step 1 zeroes the resident kernel's sync words and poisons plane 1 (its hand-off)
         r1.a.zero_words = P.a[0].sync;
         r1.a.nzero = (int)(P.sync_bytes / 4);
+        r1.a.poison = T >= 3 ? static_cast<char *>(pred_inter) + (size_t)N * es : nullptr;
     }
     if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
     if (res) {
@@ -801,10 +768,11 @@ static int launch_heads(HeadsArgs &a, void *stream) {
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 3>)};
         fn = abl[(a.dbg & 3u) - 1];
     }
-    // The attribute is per device: set it on every launch (the current device is the
-    // caller's, and DataParallel replicas launch from their own threads), as
-    // launch_resident does; a host-side call, no device work.
-    if (lds > 65536) NLSPN_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    // The attribute is per device (the current device is the caller's, and DataParallel
+    // replicas launch from their own threads): set_lds_attr makes the driver call once
+    // per device and kernel.
+    if (lds > 65536)
+        if (int rc = set_lds_attr(fn, lds)) return rc;
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kHdNT), args, (size_t)lds, as_stream(stream)));
     return check_launch("nlspn_head_epilogue");
@@ -877,9 +845,10 @@ int nlspn_propagate_normalized(int dtype, const void *p0, const void *dep, const
     const bool res = plan_resident(dtype, conf_eff, dep, aff_norm, off_ins, 2LL * (K + 1) * HW, pred_inter, pred,
                                    workspace, B, H, W, kh, kw, T, flags | kResOffInserted, P);
     StepArgs a1 = r.a;
-    if (res) {  // iteration 1 zeroes the resident kernel's progress words
+    if (res) {  // iteration 1 zeroes the resident kernel's sync words and poisons plane 1
         a1.zero_words = P.a[0].sync;
         a1.nzero = (int)(P.sync_bytes / 4);
+        a1.poison = T >= 3 ? static_cast<char *>(pred_inter) + (size_t)N * es : nullptr;
     }
     if (int rc = launch(L, a1, s)) return rc;
     if (res) return launch_resident(P, s);

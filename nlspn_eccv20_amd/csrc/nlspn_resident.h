@@ -17,30 +17,31 @@
 //   * the part's f window — every cell any valid tap of the part reads (found once:
 //     offsets are invariant), zero outside the image — lives in LDS;
 //   * per iteration only the previous depth plane moves: the window cells of
-//     p_{t-1} owned by OTHER parts are loaded (write-through hand-off, below),
-//     multiplied by conf' into the window, the taps are sampled exactly as
-//     prop_step_kernel does (same IEEE sequence: bit-identical), and p_t is stored.
+//     p_{t-1} owned by OTHER parts are loaded (hand-off, below), multiplied by conf'
+//     into the window, the taps are sampled exactly as prop_step_kernel does (same
+//     IEEE sequence: bit-identical), and p_t is stored.
 //     Rectangular parts keep that staging to the window's rim: at C2 about a
 //     third of the cells a full-width row band would restage.
 //
-// Between iterations a part waits only for the parts its window (and any
-// out-of-window tap) reads — a rectangle of parts of its own image, computed once
-// from the invariant offsets — through per-workgroup progress words.  Hand-off
-// protocol (cdna_hip_programming.md §6 Guideline 16, the write-through row of
-// MI355X_MICROARCH.md § inter-workgroup visibility):
-//   producer: every p_t store is `sc1` (write-through), every wave drains
-//             (s_waitcnt vmcnt(0)), workgroup barrier, ONE lane stores its
-//             progress word = epoch + t + 1 (relaxed, agent scope = sc1 store);
-//   consumer: ONE wave polls the words it depends on (relaxed sc1 loads),
-//             workgroup barrier, then EVERY load of a pred_inter plane is an
-//             `sc1` load (no acquire fence needed, L1 bypassed).
-// Loads of bytes not written in this launch (conf', invariants) are plain.
-// Every plane t is written once, so there is no write-after-read hazard and a
-// fast part may run ahead of parts that do not feed it.  Image groups run in turn
-// inside one launch (ResArgs::ngroups; a part sets up group k + 1 as soon as it has
-// published its last iteration of group k, while other parts still finish group k);
-// group k's progress values start at epoch = k * (T + 1), above everything group k-1
-// left in the words, so the words are zeroed once per section (by step 1).
+// Hand-off: the data is the flag (the R2 form of cdna_hip_programming.md §6 Guideline 16,
+// with a poison value as the "not yet" tag).  Every plane p_t a later iteration reads is
+// POISONED — kResPoison32 / kResPoison16, signalling-NaN bit patterns that no arithmetic
+// result has (IEEE mode quiets every NaN an instruction returns) — before it is written:
+// plane 1 by step 1 (the kernel boundary orders it), plane t + 1 by each part for its own
+// quads during iteration t, acknowledged (s_waitcnt vmcnt(0)) before the part stores plane
+// t.  A consumer re-loads each cell it stages until it is not the poison.  Why a value that
+// is not the poison is this call's p_t: the consumer read the same producer's cells of
+// plane t - 1 one iteration earlier (the window and every tap are invariant, so a part
+// reads the same cells every iteration) and waited for them, and the producer had made
+// plane t's poison visible before it stored those (induction from plane 1).  Stores:
+// `sc1` (write-through; MI355X_MICROARCH.md § inter-workgroup visibility); an image whose
+// parts all run on one XCD (kResL2): plain, the lines stay in that XCD's L2.  Loads of p:
+// `sc1` (L1 bypassed).  Loads of bytes not written in this launch (conf', invariants) are
+// plain.  Every plane is written once per call, so there is no write-after-read hazard, a
+// part never waits for a whole neighbour part (only for the cells it stages), and a fast
+// part may run ahead of parts that do not feed it.  Image groups run in turn inside one
+// launch (ResArgs::ngroups; a part sets up group k + 1 as soon as it has stored its last
+// iteration of group k, while other parts still finish group k).
 //
 // Residency: G = B * gy * gx workgroups, at most one per CU (the dynamic LDS
 // request exceeds half a CU's LDS) and G <= CU count, so the whole grid is
@@ -71,32 +72,22 @@ struct ResArgs {
     const void *off;    // offsets, batch stride off_bs: raw 2K planes, or inserted 2(K+1) (flags kResOffInserted)
     void *pred_inter;   // plane (t, b) at t * tstride + b * H * W: iteration t reads t-1, writes t
     void *pred;         // planes H*W apart: max(p_T, 0) (nlspnmodel.py:375-377)
-    unsigned *sync;     // [0] abort word, [1 + blockIdx] progress words; zeroed by step 1
+    unsigned *sync;     // [0] abort word, per part a line with its XCC id (+1); zeroed by step 1
     unsigned *status;   // host-mapped sticky abort flag of the device (nlspn_resident_status), or null
     long long off_bs;   // elements
     long long tstride;  // elements between iteration planes (B_section * H * W)
     int B, H, W, T;     // B: images of this launch
     int gy, gx;         // parts per image: gy row bands x gx quad-column bands
     int win_cells;      // LDS cells per copy of the f window: res_win_cells(blockDim.x)
-    unsigned epoch;     // progress-word base of this launch (k * (T + 1) for image group k)
+    unsigned epoch;     // tag base of this launch's XCC-id words (k * (T + 1) for image group k)
     unsigned flags;
-    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no wait, 2 no staging, 4 no taps,
-                        // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then invalid),
-                        // 32 part 0 aborts at its first wait (tests of the error reporting)
-    // flags kResFirst only: iteration 1 and the forward prologue run in this launch
-    // (no step-1 kernel).  `aff` / `conf` are then OUTPUTS written by the setup
-    // (aff_out, conf_out), and `off` holds the raw offsets.
-    const void *pinit;     // pred_init planes (H*W apart)
-    const void *conf_raw;  // raw confidence planes, or null (conf_prop off)
-    const void *aff_raw;   // raw affinity, K planes per item, batch stride aff_bs
-    long long aff_bs;      // elements
-    void *off_out;         // inserted offsets, 2(K+1) planes per item, contiguous, or null
-    const float *gamma;    // device, 1 float (aff_scale_const)
-    int kind;              // affinity kind (kAff*)
+    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no spin on staged cells, 2 no staging,
+                        // 4 no taps, 8 trace: s_memrealtime stamps per part and iteration into `pred`
+                        // (then invalid), 32 part 0 aborts at its first staging (tests of the error path)
     // image groups this launch runs in turn (0 or 1: one).  Group g is images
-    // g*B .. g*B + B - 1 from the base pointers above, with progress values from
-    // epoch + g (T + 1): a part starts group g + 1 as soon as it has published its last
-    // iteration of group g, with no launch boundary between the groups.
+    // g*B .. g*B + B - 1 from the base pointers above: a part starts group g + 1 as soon
+    // as it has stored its last iteration of group g, with no launch boundary between the
+    // groups.
     int ngroups;
 };
 
@@ -120,6 +111,13 @@ constexpr int kResPF = NLSPN_RES_PF;
 #ifndef NLSPN_RES_EXP
 #define NLSPN_RES_EXP 0  // timing experiments only (tools/res_trace.py): 1 no gathers, 2 no tap arithmetic
 #endif
+#ifndef NLSPN_RES_FMA
+#define NLSPN_RES_FMA 0  // timing experiment only: contracted bilinear (not the oracle's arithmetic)
+#endif
+#ifndef NLSPN_RES_WTRACE
+#define NLSPN_RES_WTRACE 0  // trace builds: per-wave stamps too (they cost the loop 16 B/lane of scratch)
+#endif
+constexpr bool kResWTrace = NLSPN_RES_WTRACE;
 constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, quad columns
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
 constexpr int kResCtl = 8;                       // LDS control words ahead of the window
@@ -148,16 +146,16 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 #endif
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
-constexpr unsigned kResFirst = 0x200u;            // ResArgs::flags: iteration 1 + the prologue in this launch
 constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
 // The sync workspace: one 128-B line per word group — [0] the abort word, then per part
-// i (blockIdx) the line kResLine * (1 + i) holding its progress word and (word + 1) its
-// XCC id + 1.  No two parts share a line, so a line is only ever written from one XCD.
+// i (blockIdx) the line kResLine * (1 + i) holding (word + 1) its tagged XCC id.  No two
+// parts share a line, so a line is only ever written from one XCD.
 constexpr int kResLine = 32;
-
-// Band i of n over a length L owns [i*L/n, (i+1)*L/n); owner(v) is the largest i
-// with floor(i*L/n) <= v.
-__device__ __forceinline__ int res_owner(int v, int L, int n) { return (int)(((long long)(v + 1) * n - 1) / L); }
+// "not yet written" values of the handed-off planes (nlspn_step.h kPoison32 / kPoison16,
+// also stored by step 1): signalling NaNs (quiet bit clear), which no arithmetic result is
+// (an instruction returns a NaN quieted), so a computed p_t never equals them
+constexpr unsigned kResPoison32 = kPoison32;
+constexpr unsigned short kResPoison16 = kPoison16;
 
 // q = k / d for 0 <= k < 2^22, d >= 1, by the float reciprocal rd = 1/d plus one
 // correction step (the product is within 1 of the quotient at these sizes).
@@ -185,6 +183,13 @@ __device__ __forceinline__ void res_span_merge(int *ctl, bool on, int mn, int mx
     }
 }
 
+// The trace's per-wave stamp pair of iteration t (dbg 8): after every part's five stamps
+// per iteration, 12 pairs per part and iteration; wb = the wave's first thread (uniform)
+__device__ __forceinline__ unsigned long long *res_wtrace(void *pred, int T, unsigned wb, int t) {
+    return reinterpret_cast<unsigned long long *>(pred) + (size_t)gridDim.x * T * 5 +
+           ((size_t)blockIdx.x * T + t) * 24 + 2 * (wb >> 6);
+}
+
 // A value as storage type T holds it (fp32: itself; fp16: rounded), back in fp32.
 template <typename T> __device__ __forceinline__ float round_to(float v);
 template <> __device__ __forceinline__ float round_to<float>(float v) { return v; }
@@ -206,6 +211,26 @@ template <> struct ResVec<float> {
     static __device__ __forceinline__ float load1(rsrc_t r, unsigned vo, unsigned so) {
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, AUX));
     }
+    // a handed-off quad: false while any element is the poison (then v is not this call's)
+    template <unsigned AUX>
+    static __device__ __forceinline__ bool load_p(rsrc_t r, unsigned vo, float (&v)[4]) {
+        // (whole-vector casts only: DESIGN.md §3.1, compiler pitfall)
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0u, AUX);
+        const f32x4 f = __builtin_bit_cast(f32x4, q);
+        v[0] = f[0]; v[1] = f[1]; v[2] = f[2]; v[3] = f[3];
+        return q[0] != kResPoison32 && q[1] != kResPoison32 && q[2] != kResPoison32 && q[3] != kResPoison32;
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ float load1_p(rsrc_t r, unsigned vo, bool &ready) {
+        const unsigned q = __builtin_amdgcn_raw_buffer_load_b32(r, vo, 0u, AUX);
+        ready = q != kResPoison32;
+        return __builtin_bit_cast(float, q);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void poison(rsrc_t r, unsigned vo) {
+        const u32x4 q = {kResPoison32, kResPoison32, kResPoison32, kResPoison32};
+        __builtin_amdgcn_raw_buffer_store_b128(q, r, vo, 0u, AUX);
+    }
 };
 template <> struct ResVec<__half> {
     template <unsigned AUX>
@@ -225,6 +250,28 @@ template <> struct ResVec<__half> {
         const unsigned at = vo + so;
         const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(r, at & ~3u, 0u, AUX);
         return (float)__builtin_bit_cast(_Float16, (unsigned short)((at & 2u) ? (w >> 16) : (w & 0xffffu)));
+    }
+    // the poison tests read the halves' bits (a conversion would quiet the signalling NaN)
+    template <unsigned AUX>
+    static __device__ __forceinline__ bool load_p(rsrc_t r, unsigned vo, float (&v)[4]) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, vo, 0u, AUX);
+        const f16x4 f = __builtin_bit_cast(f16x4, q);
+        v[0] = (float)f[0]; v[1] = (float)f[1]; v[2] = (float)f[2]; v[3] = (float)f[3];
+        const unsigned P2 = (unsigned)kResPoison16;
+        return (q[0] & 0xffffu) != P2 && (q[0] >> 16) != P2 && (q[1] & 0xffffu) != P2 && (q[1] >> 16) != P2;
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ float load1_p(rsrc_t r, unsigned vo, bool &ready) {
+        const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(r, vo & ~3u, 0u, AUX);
+        const unsigned short h = (unsigned short)((vo & 2u) ? (w >> 16) : (w & 0xffffu));
+        ready = h != kResPoison16;
+        return (float)__builtin_bit_cast(_Float16, h);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void poison(rsrc_t r, unsigned vo) {
+        const unsigned w = (unsigned)kResPoison16 | ((unsigned)kResPoison16 << 16);
+        const u32x2 q = {w, w};
+        __builtin_amdgcn_raw_buffer_store_b64(q, r, vo, 0u, AUX);
     }
 };
 
@@ -291,11 +338,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const bool preserve = (a.flags & kPreserve) != 0;
     const bool clip = (a.flags & kAlwaysClip) != 0;
     const bool off_ins = (a.flags & kResOffInserted) != 0;
-    const bool fused = (a.flags & kResFirst) != 0;  // iteration 1 (t = 0 below) and the prologue here
     const long long HW = (long long)H * W;
     const unsigned plane_bytes = (unsigned)HW * ES;
     const int b = bl + grp * a.B;
-    const unsigned epoch = a.epoch + (unsigned)grp * (unsigned)(a.T + 1);
 
     // ---- own quad and its invariants.  Taps are held as their sample coordinates
     // (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw), the reference's own
@@ -304,8 +349,16 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     unsigned long long *trace0 = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                    (size_t)blockIdx.x * a.T * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
+    // trace: per wave and iteration two more stamps (taps + stores issued, stores drained)
+    // after the parts' five, 24 per part and iteration (wave-uniform addresses, res_wtrace);
+    // row t = 0 holds each wave's HW_ID
+    if (kResWTrace && trace0 && (threadIdx.x & 63) == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        res_wtrace(a.pred, a.T, __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u), 0)[0] = hw;
+    }
     const bool active = tid < nown;
-    // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned, not fused): every
+    // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned): every
     // part publishes the XCC it runs on; if all parts of its image share one, the image's
     // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed: the word
     // is tagged with this launch (its epoch + 1, above the 5-bit XCC field), and a reader
@@ -313,7 +366,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // unmerged groups, trace mode) never decides from the previous launch's placement.
     // The words are zeroed once per section (step 1), and a section's launches have
     // distinct epochs.
-    const bool l2try = (a.flags & kResL2) != 0 && !fused;
+    const bool l2try = (a.flags & kResL2) != 0;
     unsigned xcc_self = 0;
     const unsigned xtag = (a.epoch + 1u) << 5;
     if (l2try) {
@@ -336,13 +389,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     {
         float dv[4];
         float ak[K][4], aref[4];
-        // fused: the raw K-plane affinity, normalised below (step 1's prologue)
-        const rsrc_t ra_ = fused ? make_rsrc(static_cast<const T *>(a.aff_raw) + (long long)b * a.aff_bs)
-                                 : make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
+        const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(fused ? k : (k < REF ? k : k + 1)) * plane_bytes, ak[k]);
+            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, ak[k]);
             const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
@@ -350,62 +401,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) dv[e] = 0.f;
         if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
-        // conf (raw when fused) with the other loads: one round trip before the stores below
         float cq[4] = {1.f, 1.f, 1.f, 1.f};
-        if (has_conf)
-            ResVec<T>::template load<0>(
-                make_rsrc(static_cast<const T *>(fused ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
-        // The output-dict offsets (_off_insert, nlspnmodel.py:324; streamed, never re-read)
-        // from the raw offsets just loaded, with the fused prologue.  (Writing them here in
-        // place of step 1 was measured slower: the 40 MB store burst delays the setup's
-        // invariant loads by 9 us where step 1 saves 6, profiles/r03/ab_offout_v1_*.txt.)
-        if (fused && active && a.off_out) {
-            const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
-            const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        if (has_conf) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), vpix, 0u, cq);
 #pragma unroll
-            for (int c = 0; c < K + 1; ++c) {
-                const int k = c < REF ? c : c - 1;
-                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
-                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
-            }
-        }
-        if (fused) {
-            // step 1's prologue for the own quad (nlspn_step.h FIRST): the normalised
-            // affinity (_affinity_normalization + _aff_insert) and, below, conf'
-            normalize_taps<K, 4>(ak, aref, a.kind, *a.gamma);
-            if (active) {
-                const rsrc_t rao = make_rsrc(static_cast<T *>(const_cast<void *>(a.aff)) + (long long)b * (K + 1) * HW);
+        for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
+            float s = 0.f;
 #pragma unroll
-                for (int c = 0; c < K + 1; ++c)
-                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, c == REF ? aref : ak[c < REF ? c : c - 1]);
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
-                float s = 0.f;
-#pragma unroll
-                for (int k = 0; k < K; ++k) s += ak[k][e];
-                aref[e] = 1.0f - s;
-            }
+            for (int k = 0; k < K; ++k) s += ak[k][e];
+            aref[e] = 1.0f - s;
         }
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
 #pragma unroll
         for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
         akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-        if (has_conf && fused) {
-            // conf' = (1-m) conf + m (:341-348), stored write-through: other parts stage it
-            // from iteration 2 on (sc1 loads below), after this part's first publish
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float m = dv[e] > 0.f ? 1.f : 0.f;
-                cq[e] = preserve ? (1.0f - m) * cq[e] + m : cq[e];
-            }
-            if (active)
-                ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(const_cast<void *>(a.conf)) + b * HW), vpix, 0u, cq);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) cq[e] = round_to<T>(cq[e]);  // as stored (the staging reloads it)
-        }
         akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
         akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
     }
@@ -414,8 +423,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (offsets are invariant, so once), when it fits the LDS cells allocated;
     // otherwise the part +- (RY rows, RXQ quads), and the rare taps outside it take
     // the general path.  Columns are whole quads plus PADX zero columns each side.
-    // The setup's barriers order LDS only (lds_barrier): global stores of the fused
-    // prologue stay in flight behind them.
+    // The setup's barriers order LDS only (lds_barrier).
     // The own rectangle plus one row and one column: the reference tap's four-corner
     // footprint (read when the window holds a non-finite f, below).  ctl[6] / ctl[7]: the
     // per-iteration "window holds a non-finite f" flags (by iteration parity).
@@ -474,12 +482,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     //    weights (1,0,0,0): v = +0 exactly, as the reference's val = 0;
     //  * in the LDS window: the branch-free path;
     //  * valid but outside the window (only with the fixed halo): read from global
-    //    memory by the general path (has_fb); the dependency rectangle covers it.
+    //    memory by the general path (has_fb), the same cells every iteration.
     // With the dynamic window no valid tap is outside it, so only the redirect of invalid
     // taps runs then (the whole pass took 4.2 us of the C2 setup, profiles/r04).
     bool has_fb = false;
     if (!dynwin) {
-        int mn = H, mx = -1, cmn = W, cmx = -1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
@@ -488,13 +495,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                     const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
                     if (!((unsigned)(h_low - rlo) < (unsigned)(WH - 1) &&
-                          (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1))) {
+                          (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)))
                         has_fb = true;
-                        mn = min(mn, max(h_low, 0));
-                        mx = max(mx, min(h_low + 1, H - 1));
-                        cmn = min(cmn, max(w_low, 0));
-                        cmx = max(cmx, min(w_low + 1, W - 1));
-                    }
                 } else {
                     hy[k][e] = (float)rlo;
                     hx[k][e] = (float)(4 * wq0 - PADX);
@@ -502,8 +504,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
         has_fb = has_fb && active;
-        res_span_merge(ctl, has_fb, mn, mx, cmn, cmx);
-        lds_barrier();
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -517,10 +517,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
     }
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
-    // the parts this one reads: a rectangle of the image's part grid
-    const int dy0 = res_owner(ctl[1], H, a.gy), dy1 = res_owner(ctl[2], H, a.gy);
-    const int dx0 = res_owner(ctl[3] >> 2, W4, a.gx), dx1 = res_owner(ctl[4] >> 2, W4, a.gx);
-    const int ndx = dx1 - dx0 + 1, ndep = (dy1 - dy0 + 1) * ndx;
     const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
     // Every tap's bilinear geometry is iteration-invariant, so it is resolved once:
     // the fractional parts lh = h - floor(h), lw = w - floor(w) (.cuh:35-36, the same
@@ -567,104 +563,51 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const rsrc_t rcg = make_rsrc(has_conf ? static_cast<const T *>(a.conf) + b * HW : p_all);
     const int lown = (y - rlo) * WW + x0 - 4 * wq0 + PADX;  // window cell of the own quad's first pixel
 
-    // Iteration t reads plane t-1 and writes plane t; fused: t = 0 is iteration 1, whose
-    // source is built from the raw inputs (p0 * conf', nlspn_step.h make_f<true>).  A part
-    // publishes epoch + t + 1 after iteration t, so iteration t waits for epoch + t; the
-    // first iteration of a launch waits for nothing (its source is an input).
-    const int t0 = fused ? 0 : 1;
-    // The polling wave: the last one holding quads, not wave 0, whose lane 0 stores the
-    // progress word — a poll load queues behind that write-through store in its wave's
-    // vmcnt order, so polling from wave 0 added the store's round trip to every wait
-    // (same-box A/B: C2 134.0k vs 124.1k iters/s, trace wait 0.96 vs 1.56 us)
+    // Iteration t (1 .. T-1: the section's iterations 2 .. T) reads plane t-1 and writes
+    // plane t.  Plane 0 is step 1's output (the launch's input: never poisoned), so the
+    // first iteration stages without waiting.  The XCC ids are read by the last wave holding
+    // quads (any wave would do).
     const int pwave = (nown - 1) >> 6;
     bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in the first iteration)
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
-    for (int t = t0; t < a.T; ++t) {
-        unsigned long long *trace = ((a.dbg & 8u) && t > 0) ? reinterpret_cast<unsigned long long *>(a.pred) +
-                                                                 ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
+    int t_abort = 0;
+    for (int t = 1; t < a.T; ++t) {
+        unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
+                                                       ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
-        const bool first = t == 0;  // fused iteration 1: f = p0 * conf' from the raw inputs
-        const T *p_in = first ? static_cast<const T *>(a.pinit) + b * HW : p_all + (size_t)(t - 1) * a.tstride + b * HW;
-        const rsrc_t rp = make_rsrc(p_in);
+        const rsrc_t rp = make_rsrc(p_all + (size_t)(t - 1) * a.tstride + b * HW);
         // ---- a launch's first iteration: the hand-off mode of this image (all its parts
         // on this part's XCC: L2), decided from the published XCC ids, identically by
-        // every part of the image; its stores at the end of this iteration use it
-        if (t == t0 && (tid >> 6) == pwave) {
-            bool same = l2try, fail = false;
-            unsigned spins = 0;
-            for (int base = 0; base < nparts && same && !fail; base += 64) {
-                const int jj = base + lane;
-                gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
-                unsigned v;
-                for (;;) {
-                    v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all((v & ~31u) == xtag)) break;
-                    if (++spins > kResSpinLimit) { fail = true; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                same = same && __all(v == (xtag | xcc_self));
-            }
-            if (lane == 0) ctl[5] = same && !fail ? 1 : 0;
-        }
-        // ---- wait until every part this one reads has finished iteration t-1
-        if (t > t0 && (tid >> 6) == pwave && !(a.dbg & 1u)) {
-            unsigned spins = 0;
-            bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
-            const unsigned need = epoch + (unsigned)t;
-            for (int base = 0; base < ndep && !fail; base += 64) {
-                const int d = base + lane;
-                const int dy = d / ndx;
-                const int jj = (dy0 + dy) * a.gx + dx0 + (d - dy * ndx);
-                // lanes without a dependency watch the abort word in the same wave load,
-                // so a spin is ONE memory round trip (a separate abort load per spin, issued
-                // after the ballot, doubled the poll period)
-                const bool spare = base + 64 > ndep;
-                gu32 *wp = d < ndep ? &sync[kResLine * (1 + xcd_unmap(bl * nparts + jj, G))] : &sync[0];
-                for (;;) {
-                    const unsigned v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all(d >= ndep || v >= need)) break;
-                    if (__any(d >= ndep && v != 0u) || ++spins > kResSpinLimit ||
-                        (!spare && (spins & 15u) == 0u &&
-                         __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-                        fail = true;
-                        break;
+        // every part of the image; its stores use it
+        if (t == 1) {
+            if ((tid >> 6) == pwave) {
+                bool same = l2try, fail = false;
+                unsigned spins = 0;
+                for (int base = 0; base < nparts && same && !fail; base += 64) {
+                    const int jj = base + lane;
+                    gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
+                    unsigned v;
+                    for (;;) {
+                        v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (__all((v & ~31u) == xtag)) break;
+                        if (++spins > kResSpinLimit) { fail = true; break; }
+                        __builtin_amdgcn_s_sleep(1);
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    same = same && __all(v == (xtag | xcc_self));
                 }
+                if (lane == 0) ctl[5] = same && !fail ? 1 : 0;
             }
-            if (fail && lane == 0) {
-                ctl[0] = 1;
-                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        // also orders the previous iteration's LDS reads before the restaging.  A launch's
-        // first iteration needs LDS order only: the setup's output stores (fused prologue)
-        // keep draining under its staging and taps, until its publish
-        if (t > t0) __syncthreads();
-        else lds_barrier();
-        if (t == t0) l2 = __builtin_amdgcn_readfirstlane(ctl[5]) != 0;
-        if (ctl[0]) {  // aborted: NaN in every plane this part has not written (this group's
-                       // remaining iterations, every later group's), then exit
-            if (active) {
-                const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
-                for (int g2 = grp; g2 < ngroups; ++g2) {
-                    const int b2 = bl + g2 * a.B;
-                    for (int tt = g2 == grp ? t : t0; tt < a.T; ++tt)
-                        ResVec<T>::template store<0>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u,
-                                                     qn);
-                    ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
-                }
-            }
-            return;
+            lds_barrier();
+            l2 = __builtin_amdgcn_readfirstlane(ctl[5]) != 0;
         }
         if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
 
-        // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads
-        // (written by other parts in this launch), conf' by plain loads (invariant)
-        // after a launch's first iteration the own quads are in the window already
-        // (written back below), so only the other parts' quads are loaded
-        const bool rim = t > t0;
+        // ---- stage f = p_{t-1} * conf' for the in-image window cells: p by sc1 loads,
+        // re-loaded until not the poison (written by other parts in this launch), conf' by
+        // plain loads (invariant).  After a launch's first iteration the own quads are in the
+        // window already (written back below), so only the other parts' quads are loaded.
+        const bool rim = t > 1;
+        const bool spin = rim && !(a.dbg & 1u);
         // the staging index (= tid) rebuilt per iteration from the wave's base (an SGPR) and
         // the lane id, so no VGPR holds it across the loop (it was spilled and reloaded)
         const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -673,6 +616,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
             int sl[SMAX];
+            unsigned gq[SMAX];
+            bool ok = true;  // every staged quad of this lane holds this call's values
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
                 const int k = base + s * NT;
@@ -687,33 +632,31 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     c = cc < left ? qa + cc : c1 + cc - left;
                 }
                 sl[s] = (r - rlo) * WW + 4 * (c - wq0) + PADX;  // window cell, % 4 == 0
+                gq[s] = (unsigned)(r * W + 4 * c) * ES;
                 if (k < nsq_it) {
-                    const unsigned go = (unsigned)(r * W + 4 * c) * ES;
-                    if (first) {  // inputs of the launch: plain loads; p0 and conf' built below
-                        ResVec<T>::template load<0>(rp, go, 0u, sv[s]);
-                        if (has_conf)
-                            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf_raw) + b * HW), go, 0u, cv[s]);
-                        if (preserve) {
-                            float dq[4];
-                            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), go, 0u, dq);
+                    ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
+                    if (has_conf) ResVec<T>::template load<0>(rcg, gq[s], 0u, cv[s]);
+                }
+            }
+            if (spin) {  // this wave's lanes re-load the quads still poisoned (a bounded spin)
+                bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
+                unsigned spins = 0;
+                while (!fail && __builtin_amdgcn_ballot_w64(!ok) != 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (!ok) {
+                        ok = true;
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) {  // make_f<true> (nlspn_step.h), conf' folded into cv
-                                const float m = dq[e] > 0.f ? 1.f : 0.f;
-                                sv[s][e] = (1.0f - m) * sv[s][e] + m * dq[e];
-                                if (has_conf) cv[s][e] = (1.0f - m) * cv[s][e] + m;
-                            }
-                        }
-                        if (clip) {
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) sv[s][e] = clamp0(sv[s][e]);
-                        }
-                    } else {
-                        ResVec<T>::template load<kSc1>(rp, go, 0u, sv[s]);
-                        if (has_conf) {  // conf' written in this launch (fused): write-through hand-off
-                            if (fused) ResVec<T>::template load<kSc1>(rcg, go, 0u, cv[s]);
-                            else ResVec<T>::template load<0>(rcg, go, 0u, cv[s]);
-                        }
+                        for (int s = 0; s < SMAX; ++s)
+                            if (base + s * NT < nsq_it) ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
                     }
+                    if (++spins > kResSpinLimit ||
+                        ((spins & 15u) == 0u && __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u))
+                        fail = true;
+                }
+                if (fail) {
+                    ctl[0] = 1;
+                    __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
 #pragma unroll
@@ -735,12 +678,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
         }
+        if (kResWTrace && trace && lane == 0) res_wtrace(a.pred, a.T, wbase, t)[1] = __builtin_amdgcn_s_memrealtime();
         if (__builtin_amdgcn_ballot_w64(nonfin) != 0 && lane == 0) ctl[6 + (t & 1)] = 1;
         lds_barrier();
         if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
+        if (ctl[0]) {  // aborted (a spin timed out, or another part's abort): below the loop
+            t_abort = t;
+            break;
+        }
         // the window holds a non-finite f (staged now, or an own quad written back after
         // the previous iteration): the reference tap takes the four-corner form below
         const bool refull = __builtin_amdgcn_readfirstlane(ctl[6 + (t & 1)]) != 0;
+        T *p_out = p_out_all + (size_t)t * a.tstride + b * HW;
+        // plane t + 1 is read by iteration t + 2 (if any): its own quad poisoned now, the
+        // store acknowledged before plane t's store below (the hand-off's ordering)
+        if (active && t + 2 < a.T) {
+            if (l2) ResVec<T>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
+            else ResVec<T>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
+        }
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
         // The tap geometry depends only on the (invariant) coordinates, so the
@@ -818,13 +773,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #if NLSPN_RES_EXP == 2  // timing experiment: gathers only, minimal arithmetic (wrong results)
                 (void)w1; (void)w2; (void)w3; (void)w4;
                 acc[e] += (s01.x + s01.y) + (s23.x + s23.y);
+#elif NLSPN_RES_FMA  // timing experiment: contracted bilinear (differs from the oracle)
+                float v = w1 * s01.x;
+                v = __builtin_fmaf(w2, s01.y, v);
+                v = __builtin_fmaf(w3, s23.x, v);
+                v = __builtin_fmaf(w4, s23.y, v);
+                acc[e] = __builtin_fmaf(v, av[e], acc[e]);
 #else
                 const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                 acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
 #endif
             }
             // general path (rare; only waves holding a tap outside the window): the
-            // reference's per-corner checks, from global memory where needed.  It
+            // reference's per-corner checks, from global memory where needed (the same
+            // cells every iteration, re-loaded until not the poison, as the staging's).  It
             // re-reads its offsets from global memory and runs a rolled tap loop, so it
             // shares no registers with the branch-free path (no spills around it).
             if (kResGeneralPath && wave_fb && has_fb) {
@@ -870,20 +832,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                     c4[u] = 0.f;
                                     if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
                                         const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                        if (first) {  // fetch_f<FIRST> of nlspn_step.h
-                                            const float pv = ResVec<T>::template load1<0>(rp, qo, 0u);
-                                            const float cr = has_conf ? ResVec<T>::template load1<0>(
-                                                make_rsrc(static_cast<const T *>(a.conf_raw) + b * HW), qo, 0u) : 1.f;
-                                            const float dr = preserve ? ResVec<T>::template load1<0>(
-                                                make_rsrc(static_cast<const T *>(a.dep) + b * HW), qo, 0u) : 0.f;
-                                            c4[u] = make_f<true>(pv, cr, dr, has_conf, preserve, clip);
-                                        } else {
-                                            const float pv = ResVec<T>::template load1<kSc1>(rp, qo, 0u);
-                                            const float cg = !has_conf ? 1.f
-                                                             : fused ? ResVec<T>::template load1<kSc1>(rcg, qo, 0u)
-                                                                     : ResVec<T>::template load1<0>(rcg, qo, 0u);
-                                            c4[u] = has_conf ? pv * cg : pv;
+                                        float pv = 0.f;
+                                        for (unsigned sp = 0;; ++sp) {  // per lane, bounded
+                                            bool rdy;
+                                            pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
+                                            if (rdy || t == 1 || (a.dbg & 1u) || sp > kResSpinLimit) break;
+                                            __builtin_amdgcn_s_sleep(1);
                                         }
+                                        c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
                                     }
                                 }
                                 v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
@@ -922,7 +878,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 o[e] = vv;
                 fin[e] = clip ? vv : clamp0(vv);  // :375-377
             }
-            T *p_out = p_out_all + (size_t)t * a.tstride + b * HW;
+            // plane t + 1's poison acknowledged first (issued before the taps: no wait left)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (l2) ResVec<T>::template store<0>(make_rsrc(p_out), vpix, 0u, o);  // kept in the XCD's L2
             else ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
 #pragma unroll
@@ -930,37 +887,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (t == a.T - 1 && !(a.dbg & 8u))
                 ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
         }
-        // ---- publish: every wave drains its write-through stores, then ONE lane
         if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (kResWTrace && trace && lane == 0) res_wtrace(a.pred, a.T, wbase, t)[0] = __builtin_amdgcn_s_memrealtime();
+        // ---- every tap of iteration t is done: the window may change
+        lds_barrier();
         if (trace && tid == 0) trace[4] = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0) {
-            ctl[6 + (t & 1)] = 0;  // every tap of iteration t is done (the barrier above)
-            gu32 *pw = &sync[kResLine * (1 + blockIdx.x)];
-            if (l2)  // same-XCD consumers only: a plain store, the line stays in the XCD's L2
-                __hip_atomic_store(pw, epoch + (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-                __hip_atomic_store(pw, epoch + (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if constexpr (ES == 2) {
-            // fused, fp16: iteration 1 used the normalised affinity unrounded (as step 1
-            // does); the later iterations use it as stored (aff_out), reference weight
-            // 1 - sum of the stored taps (the step kernel's non-first arithmetic)
-            if (first && active) {
-                float s4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    float4 v = akl[k];
-                    v.x = round_to<T>(v.x); v.y = round_to<T>(v.y); v.z = round_to<T>(v.z); v.w = round_to<T>(v.w);
-                    akl[k] = v;
-                    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
-                }
-                akl[K] = make_float4(1.0f - s4[0], 1.0f - s4[1], 1.0f - s4[2], 1.0f - s4[3]);
-            }
-        }
-        // ---- the own quad's f_t = p_t * conf' straight into the window (every tap of
-        // this iteration is done: the barrier above), as the next staging would load it
+        if (tid == 0) ctl[6 + (t & 1)] = 0;  // iteration t's flag, next used by iteration t + 2
+        // ---- the own quad's f_t = p_t * conf' straight into the window, as the next
+        // staging would load it
         if (t < a.T - 1 && active && !(a.dbg & 2u)) {
             const float4 cw = akl[K + 1];
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
@@ -974,6 +908,22 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (!__builtin_isfinite((f.x + f.y) + (f.z + f.w)))
                 ctl[6 + ((t + 1) & 1)] = 1;  // (benign race: every writer stores 1)
         }
+    }
+    // aborted: NaN in every plane this part has not written (this group's remaining
+    // iterations, every later group's), then exit.  Write-through: a consumer spinning on
+    // these cells takes the NaN and runs on.  (Out of the loop: its registers would cost
+    // the loop scratch.)
+    if (t_abort) {
+        if (active) {
+            const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+            for (int g2 = grp; g2 < ngroups; ++g2) {
+                const int b2 = bl + g2 * a.B;
+                for (int tt = g2 == grp ? t_abort : 1; tt < a.T; ++tt)
+                    ResVec<T>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
+                ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
+            }
+        }
+        return;
     }
     }  // image groups
 }

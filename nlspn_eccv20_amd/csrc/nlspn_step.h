@@ -61,9 +61,16 @@ struct StepArgs {
     void *off_out;       // 2(K+1) planes per item, contiguous, or null
     void *conf_out;      // B planes, or null iff conf null
     int kind;            // affinity kind
-    unsigned *zero_words;  // step 1: progress words of the resident kernel that follows, zeroed here
+    unsigned *zero_words;  // step 1: sync words of the resident kernel that follows, zeroed here
     int nzero;             //   (replaces a memset node; the kernel boundary orders it)
+    void *poison;          // step 1: plane 1 (B planes), filled with the resident hand-off's poison
+                           //   (nlspn_resident.h) for the own pixels, or null
 };
+
+// The resident kernel's "not yet written" plane values (nlspn_resident.h): signalling NaNs
+// (quiet bit clear), which no arithmetic result is
+constexpr unsigned kPoison32 = 0x7f800badu;
+constexpr unsigned short kPoison16 = 0x7d0bu;
 
 constexpr unsigned kPreserve = 0x1u;
 constexpr unsigned kAlwaysClip = 0x2u;
@@ -582,6 +589,14 @@ __global__ void __launch_bounds__(TH * TW / PX, (sizeof(T) == 2 && OFFSET && !FI
     }
     BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.p_out) + b * HW), vpix, 0u, o);
     if (a.pred_out) BVec<T, PX>::store(make_rsrc(static_cast<T *>(a.pred_out) + b * HW), vpix, 0u, fin);
+    if (a.poison) {  // raw bit stores (a float or half conversion would quiet the signalling NaN)
+        const rsrc_t rq = make_rsrc(static_cast<T *>(a.poison) + b * HW);
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+            if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(kPoison32, rq, vpix + p * ES, 0u, 0);
+            else __builtin_amdgcn_raw_buffer_store_b16(kPoison16, rq, vpix + p * ES, 0u, 0);
+        }
+    }
 }
 
 }  // namespace nlspn

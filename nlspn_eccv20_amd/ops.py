@@ -189,12 +189,15 @@ def _register_autograd() -> None:
 
     def setup_step(ctx, inputs, output):
         feat, confidence, dep, aff, offset, kh, kw, raw_offsets, preserve_input, always_clip = inputs
-        if offset is not None and not raw_offsets:
-            raise NotImplementedError("nlspn::prop_step's backward takes raw_offsets=True (B, 2K, H, W) offsets")
+        # (the inserted layout has no backward: raised in bwd_step, as _PropStepFn.backward
+        # does, so a forward with grad mode on still runs)
+        ctx.inserted = offset is not None and not raw_offsets
         ctx.save_for_backward(feat, confidence, dep, aff, offset)
         ctx.cfg = (kh, kw, preserve_input, always_clip)
 
     def bwd_step(ctx, g_out):
+        if ctx.inserted:
+            raise NotImplementedError("nlspn::prop_step's backward takes raw_offsets=True (B, 2K, H, W) offsets")
         feat, confidence, dep, aff, offset = ctx.saved_tensors
         gf, gc, ga, go = torch.ops.nlspn.prop_step_backward(feat, confidence, dep, aff, offset, g_out, *ctx.cfg)
         return (gf, gc if confidence is not None else None, None, ga, go if offset is not None else None) + \

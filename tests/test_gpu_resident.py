@@ -1,6 +1,5 @@
 """GPU: the resident propagation kernel (iterations 2..T in one launch per image
-group after a step-1 launch — or, NLSPN_RES_FIRST=1, the prologue and iterations
-1..T in the launches — invariant planes on chip, per-workgroup progress words)
+group after a step-1 launch, invariant planes on chip, poisoned-plane hand-offs)
 against the per-iteration launches and the oracle.
 
 Bar: BIT-EXACT against step 1 + the T-1 per-iteration launches (all forms issue the
@@ -65,11 +64,12 @@ def _nan_equal(x, y):
 
 def _both(inp, T=18, nan_ok=False, **kw):
     """(resident, steps): the default resident form (behind a step-1 launch), checked
-    here against the resident form with iteration 1 inside the launches, and the step form.
+    here against the resident form with every hand-off write-through (NLSPN_RES_L2=0: no
+    image's hand-offs kept in an XCD's L2), and the step form.
     nan_ok: NaN results compare by position (_nan_equal)."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
-        with _env("1", "NLSPN_RES_FIRST"):
+        with _env("0", "NLSPN_RES_L2"):
             c = propagate(*inp, prop_time=T, **kw)
     with _env("0"):
         b = propagate(*inp, prop_time=T, **kw)
@@ -242,15 +242,12 @@ def test_time_propagate_reports_resident():
         plan = PropagationPlan(*inp, prop_time=18)
         first, rest, res = timed(plan.outputs)
         assert res == 1 and first > 0 and rest > 0  # one resident launch (one image group) behind step 1
-        with _env("1", "NLSPN_RES_FIRST"):  # iteration 1 inside the resident launch: no step-1 kernel
-            first, rest, res = timed(plan.outputs)
-        assert res == 1 | _lib.RESIDENT_FIRST and first >= 0 and rest > 0
         plan.close()
 
 
 def test_c3_resident_vs_oracle_and_replays(oracle):
     """C3 (KITTI B=4) runs iterations 2..T as two image groups of two images each, in
-    turn inside one resident launch (progress words carried across them by epoch):
+    turn inside one resident launch (a part sets up group 2 while others finish group 1):
     against the oracle at the north-star bar, and stable over plan replays."""
     inp, s = _inputs(4, 240, 1216, seed=7240)
     with _env("1"):

@@ -19,18 +19,15 @@ import resource_usage as RU  # noqa: E402
 
 HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # The resident kernel runs at its 168-VGPR cap (768-thread launch bound = 3 waves per
-# SIMD) with 80 VGPRs of tap geometry held across its iteration loop.  Its spill slots
-# belong to the setup.  The GROUPS builds (several image groups in turn per launch) wrap
-# the setup in the group loop (depth 1: its slots grow), so their iteration loop sits at
-# depth 2.  Inside the iteration loop at most one reload (a staging index) is allowed —
-# checked on the kernel's device assembly, so a spill cannot come back into it silently.
-RESIDENT_SCRATCH_CAP = 64         # bytes per lane, single-group builds (setup slots)
-RESIDENT_SCRATCH_CAP_GROUPS = 192  # bytes per lane, GROUPS builds
+# SIMD) with 80 VGPRs of tap geometry held across its iteration loop.  Since round 4 (the
+# abort path moved below the iteration loop) every build compiles without scratch; a
+# spill coming back must fail here.  The GROUPS builds (several image groups in turn per
+# launch) wrap the iteration loop in the group loop, so it sits at depth 2.  The loop is
+# also checked on the kernel's device assembly: no scratch instruction inside it.
+RESIDENT_SCRATCH_CAP = 0          # bytes per lane, single-group builds
+RESIDENT_SCRATCH_CAP_GROUPS = 0   # bytes per lane, GROUPS builds
 RESIDENT_LOOP_RELOADS = 0         # scratch instructions inside the iteration loop, per instantiation
-# fp16 builds (no bench config runs them: C2 / C3 / C1 are fp32) may keep up to two 4-byte
-# reloads per iteration since round 4 (GROUPS builds; the own-quad write-back's window
-# address beside the non-finite flag of the reference tap and the interior-first split)
-RESIDENT_LOOP_RELOADS_F16 = 2
+RESIDENT_LOOP_RELOADS_F16 = 0     # the fp16 builds alike
 
 
 def _groups(name):

@@ -1,6 +1,6 @@
 """Interleaved same-process A/B of two propagation plans that differ only in one
-environment setting read at plan creation (default: NLSPN_RES_FIRST=1, the section's
-first iteration inside the resident launches, vs step 1 as its own launch).  Both
+environment setting read at plan creation (default: NLSPN_RES_L2=0, every resident
+hand-off write-through, vs same-XCD images' hand-offs kept in the XCD's L2).  Both
 plans replay on the same inputs in alternating rounds of 20, so box-to-box and drift
 noise cancel; prints the median per-section time of each per config (JSON).
 usage: python tools/ab_env.py [--rounds 15] [--env NAME=VALUE] [--configs nyu,kitti]"""
@@ -30,7 +30,7 @@ def plan_for(inputs, cfg, env):
             os.environ[name] = old
 
 
-def main(rounds=15, per=20, env="NLSPN_RES_FIRST=1", configs=("nyu", "kitti", "nyu_b1")):
+def main(rounds=15, per=20, env="NLSPN_RES_L2=0", configs=("nyu", "kitti", "nyu_b1")):
     dev = torch.device("cuda", 0)
     out = {"B": env}
     name_ = env.split("=", 1)[0]
@@ -66,7 +66,7 @@ if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=15)
-    ap.add_argument("--env", default="NLSPN_RES_FIRST=1", help="the B plan's setting")
+    ap.add_argument("--env", default="NLSPN_RES_L2=0", help="the B plan's setting")
     ap.add_argument("--configs", default="nyu,kitti,nyu_b1")
     a = ap.parse_args()
     main(a.rounds, env=a.env, configs=tuple(a.configs.split(",")))

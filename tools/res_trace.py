@@ -1,8 +1,9 @@
 """Critical-path trace of the resident kernel (NLSPN_RES_DBG=8): thread 0 of every part
-stamps s_memrealtime (100 MHz) at five points of each iteration — loop top (S0), after
-the wait barrier (S1), after staging (S2), before the drain (S3), after the publish
-barrier (S4) — into the `pred` buffer.  Prints per-phase medians (us) per image-group
-launch; "wait" is the hand-off latency plus the skew to the slowest neighbour part.
+stamps s_memrealtime (100 MHz) at five points of each iteration — loop top (S0), before
+staging (S1), after the staging barrier (S2: staging includes the spin on poisoned cells,
+i.e. the hand-off latency plus the skew to the slowest producer), taps + stores issued
+(S3), after the closing barrier (S4) — into the `pred` buffer.  Prints per-phase medians
+(us) per image-group launch.  Builds with NLSPN_RES_WTRACE=1 add per-wave stamps.
 usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1] [--bg IMAGES_PER_LAUNCH] [--out FILE]"""
 import ctypes
 import json
@@ -50,6 +51,11 @@ def main(config="nyu", T=18, reps=5, bg=None, out=None):
         o = grp * bg * HW // 2  # group k's stamps start at its own pred planes (int64 = 2 floats)
         st = allst[o: o + G * T * 5].reshape(G, T, 5).astype(np.float64) / 100.0  # us
         res[f"group{grp}"] = phases(st, G, B if ng == 1 else bg, g, T)
+        # per-wave stamps (after every part's five): [part, t, wave, (taps+stores issued, drained)]
+        wv = allst[o + G * T * 5: o + G * T * 29].reshape(G, T, 12, 2)
+        s2 = allst[o: o + G * T * 5].reshape(G, T, 5)[:, :, 2]
+        if (wv[:, 0, :, 0] != 0).any():  # builds with per-wave stamps (NLSPN_RES_WTRACE=1)
+            res[f"group{grp}"]["waves"] = waves(s2, wv)
     line = json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res})
     if out:  # the JSON alone (the runtime's stderr lines never land in the file)
         with open(out, "w") as f:
@@ -74,6 +80,18 @@ def phases(st, G, B, g, T):
     out["per_iter_us"] = round(float(span) / st.shape[1], 3)
     out["setup"] = {k: round(float(v), 3) for k, v in setup.items()}
     return out
+
+
+def waves(s2, wv):
+    """Per wave of a part: the median time (us) from the part's taps start (S2, after the
+    staging barrier) to the wave's taps + stores issued and to its stores drained, over
+    iterations 2..T, and the SIMD the wave ran on (HW_ID bits 5:4, recorded at entry)."""
+    hw = wv[:, 0, :, 0]
+    nw = int(max(1, ((hw != 0).any(0)).sum()))
+    rel = (wv[:, 1:, :nw, :].astype(np.float64) - s2[:, 1:, None, None].astype(np.float64)) / 100.0
+    return {"simd": [int(np.bincount(((hw[:, w] >> 4) & 3).astype(np.int64), minlength=4).argmax()) for w in range(nw)],
+            "issued": [round(float(np.median(rel[:, :, w, 0])), 3) for w in range(nw)],
+            "drained": [round(float(np.median(rel[:, :, w, 1])), 3) for w in range(nw)]}
 
 
 if __name__ == "__main__":
