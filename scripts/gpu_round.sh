@@ -5,7 +5,7 @@
 # usage: scripts/gpu_round.sh [TAG]   (outputs under gpurun_out/round_TAG)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r03}
+TAG=${1:-r04}
 O=$R/gpurun_out/round_$TAG
 mkdir -p $O
 cd $R
@@ -43,10 +43,18 @@ cd $R && timeout -k 10 180 python tools/head_prof.py > $O/head_prof.json 2> $O/h
 # correction on this code) and the C5 step kernel's SQ counters
 bash $R/scripts/gpu_pmc_req.sh $TAG nyu kitti nyu_b1 nyu_k16 || exit 1
 bash $R/scripts/gpu_c5_pmc.sh $TAG || exit 1
-# same-box A/B against the round's base library, when present
+# SQ counters of the resident kernel (C2) and its trace
+bash $R/scripts/gpu_sq.sh $TAG nyu > $O/sq_nyu.log 2>&1 || exit 1
+cp $R/gpurun_out/sq_${TAG}_nyu/sq_summary.json $O/sq_resident_nyu.json || exit 1
 cd $R
-if [ -f nlspn_eccv20_amd/lib/ab/libnlspn_r3base.so ]; then
+for CFG in nyu kitti nyu_b1; do
+  BG=""; [ "$CFG" = kitti ] && BG="--bg 2"
+  timeout -k 10 120 python tools/res_trace.py --config $CFG $BG --out $O/res_trace_$CFG.json > $O/res_trace_$CFG.log 2>&1 || exit 1
+done
+# same-box A/B against the round's base library (the previous round's HEAD), when present
+BASE=${AB_BASE:-nlspn_eccv20_amd/lib/ab/libnlspn_r4base.so}
+if [ -f $BASE ]; then
   for CFG in nyu kitti nyu_k16 nyu_b1; do
-    AB_CONFIG=$CFG bash scripts/gpu_ab.sh cur=- base=nlspn_eccv20_amd/lib/ab/libnlspn_r3base.so > $O/ab_$CFG.txt 2>&1 || exit 1
+    AB_CONFIG=$CFG bash scripts/gpu_ab.sh cur=- base=$BASE > $O/ab_$CFG.txt 2>&1 || exit 1
   done
 fi
