@@ -2,13 +2,16 @@
 # Round evidence on the GPU box: full GPU test suite, the default bench line (C2 headline
 # + C3 / C5 / C1 under "configs" + cpu_baseline), rocprofv3 kernel stats of the default
 # bench, and PMC HBM-traffic passes (FETCH_SIZE / WRITE_SIZE, one counter per pass).
-# usage: scripts/gpu_round.sh [TAG]   (outputs under gpurun_out/round_TAG)
+# usage: [PART=a|b] scripts/gpu_round.sh [TAG]   (outputs under gpurun_out/round_TAG; PART a =
+#        tests, bench lines and kernel stats, b = counters, traces and A/B; default both)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r04}
 O=$R/gpurun_out/round_$TAG
 mkdir -p $O
 cd $R
+PART=${PART:-ab}
+if [[ $PART == *a* ]]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
     > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
@@ -26,6 +29,9 @@ for CFG in nyu kitti nyu_k16 nyu_b1; do
       python3 $R/bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-backward --no-gru --no-heads \
       --no-extra-configs > $O/stats_$CFG.log 2>&1 || exit 1
 done
+fi
+[[ $PART == *b* ]] || exit 0
+cd /tmp && export TMPDIR=/tmp
 # PMC HBM traffic, one config per pass pair (kernels are shared between configs)
 for CFG in nyu kitti nyu_k16 nyu_b1; do
   for C in FETCH_SIZE WRITE_SIZE; do

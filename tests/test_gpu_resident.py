@@ -216,6 +216,35 @@ def test_resident_replays_stable_and_no_abort():
         plan.close()
 
 
+@pytest.mark.parametrize("B,H,W,l2,dtype", [
+    (8, 228, 304, "1", torch.float32), (8, 228, 304, "0", torch.float32), (4, 240, 1216, "1", torch.float32),
+    (1, 228, 304, "1", torch.float32), (8, 228, 304, "1", torch.float16)])
+def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype):
+    """Replays over in-place refilled inputs that alternate between two data sets: every
+    plane a hand-off reads was last written with the OTHER set's values, so a consumer that
+    took a previous call's cell instead of waiting out the poison (nlspn_resident.h) changes
+    the result.  Long-range offsets (sigma 3), L2-kept and write-through hand-offs, the
+    two-group merged launch (KITTI B=4), one image over 32 parts, fp16 storage."""
+    ia, _ = _inputs(B, H, W, sigma=3.0, seed=31, dtype=dtype)
+    ib, _ = _inputs(B, H, W, sigma=3.0, seed=32, dtype=dtype)
+    with _env("0"):
+        ra = propagate(*ia, prop_time=18)["pred_inter_tensor"].clone()
+        rb = propagate(*ib, prop_time=18)["pred_inter_tensor"].clone()
+    buf = [None if x is None else x.clone() for x in ia]
+    with _env("1"), _env(l2, "NLSPN_RES_L2"):
+        plan = PropagationPlan(*buf, prop_time=18)
+        for i in range(12):
+            src, ref = (ia, ra) if i % 2 == 0 else (ib, rb)
+            for d, x in zip(buf, src):
+                if d is not None:
+                    d.copy_(x)
+            o = plan.replay()
+            torch.cuda.synchronize()
+            assert _bits_equal(o["pred_inter_tensor"], ref), f"replay {i}"
+        plan.check()
+        plan.close()
+
+
 def test_resident_vs_oracle_c2(oracle):
     inp, s = _inputs(8, 228, 304, seed=7240)
     with _env("1"):

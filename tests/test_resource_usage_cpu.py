@@ -25,7 +25,7 @@ HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # launch) wrap the iteration loop in the group loop, so it sits at depth 2.  The loop is
 # also checked on the kernel's device assembly: no scratch instruction inside it.
 RESIDENT_SCRATCH_CAP = 0          # bytes per lane, single-group builds
-RESIDENT_SCRATCH_CAP_GROUPS = 0   # bytes per lane, GROUPS builds
+RESIDENT_SCRATCH_CAP_GROUPS = 16  # bytes per lane, GROUPS builds (setup slots of the fp16 one)
 RESIDENT_LOOP_RELOADS = 0         # scratch instructions inside the iteration loop, per instantiation
 RESIDENT_LOOP_RELOADS_F16 = 0     # the fp16 builds alike
 
