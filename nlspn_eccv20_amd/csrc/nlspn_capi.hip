@@ -399,7 +399,7 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
 // Fills P and returns true when the resident kernel applies (iterations 2..T).
 bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
-                   int kw, int T, unsigned flags, ResPlan &P, void *off_out = nullptr) {
+                   int kw, int T, unsigned flags, ResPlan &P) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
@@ -413,9 +413,9 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (HW * 9 * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into a 9-plane item
     ResShape S;
     if (!res_shape(B, H, W, cus, S)) return false;
-    if (const char *gs = getenv("NLSPN_RES_GRID")) {  // A/B only: "gy,gx" part grid (same images per launch)
+    if (const char *gs = getenv("NLSPN_RES_GRID")) {  // A/B only: "gy,gx" or "gyxgx" part grid (same images per launch)
         int gy = 0, gx = 0;
-        if (sscanf(gs, "%d,%d", &gy, &gx) == 2 && gy >= 1 && gx >= 1 && gy <= H && gx <= W / 4 &&
+        if (sscanf(gs, "%d%*c%d", &gy, &gx) == 2 && gy >= 1 && gx >= 1 && gy <= H && gx <= W / 4 &&
             S.Bg * gy * gx <= cus) {
             const int ph = (H + gy - 1) / gy, pq = (W / 4 + gx - 1) / gx, nt = (ph * pq + 63) / 64 * 64;
             if (nt <= kResMaxNT &&
@@ -430,7 +430,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if ((size_t)(G + 1) * 4 * kResLine > kSyncBytes) return false;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded)
-    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAX * (size_t)S.nt,
+    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt,
                                         80 * 1024 + 16);
     if (lds > (size_t)kResLds) return false;
     // the fixed-halo window of the largest part within the 576-thread builds' pitch / cells
@@ -451,9 +451,6 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // by two images), not with the fused prologue; NLSPN_RES_L2=0 (A/B) keeps every
     // hand-off write-through
     const char *l2env = getenv("NLSPN_RES_L2");
-    // early staging loads (nlspn_resident.h): opt-in (NLSPN_RES_EARLY=1) until measured
-    const char *eenv = getenv("NLSPN_RES_EARLY");
-    const bool early = eenv && eenv[0] == '1';
     const bool l2ok = !(l2env && l2env[0] == '0') && ((long long)HW * (long long)es) % 128 == 0 &&
                       aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
     for (int k = 0; k < ng; ++k) {
@@ -469,8 +466,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          const_cast<void *>(at(pred_inter, b0 * HW)), const_cast<void *>(at(pred, b0 * HW)),
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
                          Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)),
-                         flags | (l2ok ? kResL2 : 0u) | (early ? kResEarly : 0u), dbg,
-                         off_out ? static_cast<char *>(off_out) + (size_t)(b0 * 2 * (K + 1) * HW * (long long)es) : nullptr};
+                         flags | (l2ok ? kResL2 : 0u), dbg};
     }
     // The full image groups run in turn inside ONE launch (ResArgs::ngroups): no launch
     // boundary between them, so a part sets up its next group while others finish the
@@ -642,18 +638,12 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
 
     if (resident) *resident = 0;
     ResPlan P;
-    // the output dict's inserted offsets: written by the resident setup (streamed under its
-    // compute) instead of step 1, whose section is HBM-bound: opt-in (NLSPN_RES_OFFOUT=1)
-    // until measured
-    const char *oenv = getenv("NLSPN_RES_OFFOUT");
-    void *res_off_out = off_out && aligned(off_out, 4 * es) && (oenv && oenv[0] == '1') ? off_out : nullptr;
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
-                                   pred, workspace, B, H, W, kh, kw, T, flags, P, res_off_out);
+                                   pred, workspace, B, H, W, kh, kw, T, flags, P);
     if (res) {  // step 1 zeroes the resident kernel's sync words and poisons plane 1 (its hand-off)
         r1.a.zero_words = P.a[0].sync;
         r1.a.nzero = (int)(P.sync_bytes / 4);
         r1.a.poison = T >= 3 ? static_cast<char *>(pred_inter) + (size_t)N * es : nullptr;
-        if (res_off_out) r1.a.off_out = nullptr;  // the resident setup writes it
     }
     if ((rc = launch(L1, r1.a, s, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr))) return rc;
     if (res) {

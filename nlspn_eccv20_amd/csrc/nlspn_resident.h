@@ -84,10 +84,6 @@ struct ResArgs {
     unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no spin on staged cells, 2 no staging,
                         // 4 no taps, 8 trace: s_memrealtime stamps per part and iteration into `pred`
                         // (then invalid), 32 part 0 aborts at its first staging (tests of the error path)
-    // the output dict's inserted offsets (_off_insert, nlspnmodel.py:324), 2(K+1) planes per item,
-    // contiguous, written by the setup from the raw offsets it loads (then step 1 does not), or
-    // null.  Raw offset layout only.
-    void *off_out;
     // image groups this launch runs in turn (0 or 1: one).  Group g is images
     // g*B .. g*B + B - 1 from the base pointers above: a part starts group g + 1 as soon
     // as it has stored its last iteration of group g, with no launch boundary between the
@@ -126,14 +122,13 @@ constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, 
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
 constexpr int kResCtl = 8;                       // LDS control words ahead of the window
 constexpr int kResAS = 11;                       // float4 per thread: K = 8 affinities, 1 - sum, conf', dep
-constexpr int kResAX = kResAS + 1;               // LDS float4 per thread: those + its rim quad's conf' (rcl)
 constexpr int kResLds = 160 * 1024;              // LDS per CU
 
 // LDS cells per copy of the f window for nt threads: what the per-thread rows leave,
 // a multiple of 4 (16-B aligned copies), both copies addressable by 16-bit indices.
 __host__ __device__ constexpr int res_win_cells(int nt) {
-    return ((kResLds - 4 * kResCtl - 16 * kResAX * nt) / 8 / 4 * 4) < 32764
-               ? ((kResLds - 4 * kResCtl - 16 * kResAX * nt) / 8 / 4 * 4)
+    return ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4) < 32764
+               ? ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4)
                : 32764;
 }
 
@@ -152,7 +147,6 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
-constexpr unsigned kResEarly = 0x800u;            // ResArgs::flags: early staging loads (single-round rims)
 // The sync workspace: one 128-B line per word group — [0] the abort word, then per part
 // i (blockIdx) the line kResLine * (1 + i) holding (word + 1) its tagged XCC id.  No two
 // parts share a line, so a line is only ever written from one XCD.
@@ -315,8 +309,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (1 with conf_prop off) and dep (0 with preserve off) — every one an immediate
     // offset from ONE address register.
     float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
-    // then one float4 per thread (consecutive: conflict-free): its rim staging quad's conf'
-    float4 *rcl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)NT * kResAS + tid;
 
     gu32 *sync = (gu32 *)(a.sync);
     const int ngroups = GROUPS && a.ngroups > 1 ? a.ngroups : 1;
@@ -429,21 +421,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
         akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
         akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
-        // The output dict's inserted offsets (_off_insert, nlspnmodel.py:324), from the raw
-        // offsets just loaded: streamed (never re-read here) while the setup computes below,
-        // 40 MB at C2 that step 1 no longer writes on its HBM-bound path.  Issued after the
-        // loads have landed (the affinity rows above waited for them), so they do not
-        // delay them.
-        if (a.off_out && active && !off_ins) {
-            const rsrc_t roo = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
-            const float z[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < K + 1; ++c) {
-                const int k = c < REF ? c : c - 1;
-                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
-                ResVec<T>::template store<kNT>(roo, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
-            }
-        }
     }
 
     // ---- the window: the rectangle of every cell a valid tap of this part touches
@@ -609,21 +586,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             c = cc < left ? qa + cc : c1 + cc - left;
         }
     };
-    // Early staging (a rim of one quad per thread at most, the common case): a wave issues
-    // its next iteration's staging load right after its own taps and stores, so the load's
-    // latency runs under the closing barrier and the own write-back, and the rim quad's
-    // conf' (invariant) is held in registers from the setup on.
-    const bool early = (a.flags & kResEarly) && SMAX == 1 && nrest <= NT && !(a.dbg & 2u);
-    float pre_sv[4] = {0.f, 0.f, 0.f, 0.f};
-    bool pre_ok = true;
-    if (early && has_conf && tid < nrest) {  // (in LDS: held in registers it was spilled)
-        int r, c;
-        rim_quad(tid, r, c);
-        float cq[4];
-        ResVec<T>::template load<0>(rcg, (unsigned)(r * W + 4 * c) * ES, 0u, cq);
-        *rcl = make_float4(cq[0], cq[1], cq[2], cq[3]);
-    }
-
     // Iteration t (1 .. T-1: the section's iterations 2 .. T) reads plane t-1 and writes
     // plane t.  Plane 0 is step 1's output (the launch's input: never poisoned), so the
     // first iteration stages without waiting.  The XCC ids are read by the last wave holding
@@ -693,19 +655,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 sl[s] = (r - rlo) * WW + 4 * (c - wq0) + PADX;  // window cell, % 4 == 0
                 gq[s] = (unsigned)(r * W + 4 * c) * ES;
                 if (k < nsq_it) {
-                    if (early && rim) {  // loaded at the end of the previous iteration
-                        const float4 rc4 = *rcl;
-                        const float rcv[4] = {rc4.x, rc4.y, rc4.z, rc4.w};
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            sv[s][e] = pre_sv[e];
-                            cv[s][e] = rcv[e];
-                        }
-                        ok = pre_ok && ok;
-                    } else {
-                        ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
-                        if (has_conf) ResVec<T>::template load<0>(rcg, gq[s], 0u, cv[s]);
-                    }
+                    ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
+                    if (has_conf) ResVec<T>::template load<0>(rcg, gq[s], 0u, cv[s]);
                 }
             }
             if (spin) {  // this wave's lanes re-load the quads still poisoned (a bounded spin)
@@ -956,17 +907,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1 && !(a.dbg & 8u))
                 ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
-        }
-        // ---- early staging load of the next iteration's rim quad (plane t: other parts are
-        // storing it about now; a poisoned cell is re-loaded at the staging)
-        if (early && t + 1 < a.T) {
-            const int k = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-            if (k < nrest) {
-                int r, c;
-                rim_quad(k, r, c);
-                pre_ok = ResVec<T>::template load_p<kSc1>(make_rsrc(p_all + (size_t)t * a.tstride + b * HW),
-                                                          (unsigned)(r * W + 4 * c) * ES, pre_sv);
-            }
         }
         if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
         if (kResWTrace && trace && lane == 0) res_wtrace(a.pred, a.T, wbase, t)[0] = __builtin_amdgcn_s_memrealtime();

@@ -18,7 +18,7 @@ LDS = 160 * 1024
 
 
 def win_cells(nt):
-    return min((LDS - 4 * CTL - 16 * 12 * nt) // 8 // 4 * 4, 32764)
+    return min((LDS - 4 * CTL - 16 * 11 * nt) // 8 // 4 * 4, 32764)
 
 
 def res_shape(B, H, W, cus=256):
