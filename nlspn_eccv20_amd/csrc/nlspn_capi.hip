@@ -357,19 +357,16 @@ struct ResShape {
 // one with the least estimated work per iteration: the largest part's quads plus a
 // fifth per quad of its window rim restaged every iteration (a rim of ~9 px: the
 // 3x3 taps at N(0,2^2) offsets).  Measured weights: C2 taps 2.4 us for 542 quads,
-// staging 1.2 us for ~1350 quads.
+// staging 1.2 us for ~1350 quads.  Every CU may hold a part: with the
+// poisoned-plane hand-off (a part waits only for the cells it stages) a B=1 NYU image
+// in 247 parts runs 6 % faster than in 32 (same box, 222.0 k vs 209.2 k iters/s,
+// profiles/r04/ab_grid_nyu_b1_r04.txt) — round 2's cap of cus / 8 parts per image (fewer
+// neighbours to wait for under the flag hand-off) is gone.
 bool res_shape(int B, int H, int W, int cus, ResShape &S) {
     const int W4 = W / 4;
     const long long Q = (long long)H * W4;
-    for (int Bg = std::min(B, cus); Bg >= 1; --Bg)
-        for (int capped = 1; capped >= 0; --capped) {
-        // First at most cus / kNumXcd parts per image (C2's 32: its shape at any batch —
-        // a B=1 NYU image in 32 parts of 551 quads ran 5.6 % faster than in the 247 parts
-        // of 68 quads the cost model alone picks, profiles/r02/ab_grid_b1_*.json; the new default vs the old 13x19 grid: 110.9 vs 117.2 and 111.7 vs 122.3 us per section: fewer,
-        // larger parts depend on fewer neighbours), then as many as the CUs allow.
-        const int gcap = capped ? std::max(1, cus / kNumXcd) : cus;
-        if (capped && cus / Bg <= gcap) continue;  // the cap changes nothing
-        const int gmax = (int)std::min<long long>(std::min(cus / Bg, gcap), std::max<long long>(1, Q / 64));
+    for (int Bg = std::min(B, cus); Bg >= 1; --Bg) {
+        const int gmax = (int)std::min<long long>(cus / Bg, std::max<long long>(1, Q / 64));
         double best = 1e300;
         for (int g = gmax; g >= std::max(1, gmax * 3 / 4); --g) {
             for (int gy = 1; gy <= g; ++gy) {
@@ -392,7 +389,7 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
             }
         }
         if (best < 1e300) return true;
-        }
+    }
     return false;
 }
 

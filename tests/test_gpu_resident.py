@@ -97,8 +97,8 @@ def test_resident_engaged_at_c2():
         ok, grid, block, lds = resident_config(4, 240, 1216)  # C3: two launches of 2 images x 128 parts
         assert ok and grid == 256 and block == 576 and lds > 80 * 1024
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
-        ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in C2's 32 parts
-        assert ok and grid == 32 and block == 576
+        ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in 13 x 19 parts of 72 quads
+        assert ok and grid == 247 and block == 128
 
 
 @pytest.mark.parametrize("B,H,W,sigma,dtype,conf,kw", [

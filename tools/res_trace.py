@@ -52,10 +52,11 @@ def main(config="nyu", T=18, reps=5, bg=None, out=None):
         st = allst[o: o + G * T * 5].reshape(G, T, 5).astype(np.float64) / 100.0  # us
         res[f"group{grp}"] = phases(st, G, B if ng == 1 else bg, g, T)
         # per-wave stamps (after every part's five): [part, t, wave, (taps+stores issued, drained)]
-        wv = allst[o + G * T * 5: o + G * T * 29].reshape(G, T, 12, 2)
-        s2 = allst[o: o + G * T * 5].reshape(G, T, 5)[:, :, 2]
-        if (wv[:, 0, :, 0] != 0).any():  # builds with per-wave stamps (NLSPN_RES_WTRACE=1)
-            res[f"group{grp}"]["waves"] = waves(s2, wv)
+        if o + G * T * 29 <= allst.size:  # room for the per-wave stamps (small batches: not)
+            wv = allst[o + G * T * 5: o + G * T * 29].reshape(G, T, 12, 2)
+            s2 = allst[o: o + G * T * 5].reshape(G, T, 5)[:, :, 2]
+            if (wv[:, 0, :, 0] != 0).any():  # builds with per-wave stamps (NLSPN_RES_WTRACE=1)
+                res[f"group{grp}"]["waves"] = waves(s2, wv)
     line = json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res})
     if out:  # the JSON alone (the runtime's stderr lines never land in the file)
         with open(out, "w") as f:
