@@ -737,7 +737,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // the compiler (waits per slot), which measured faster: nine waves per CU already
             // keep the LDS array busy, and its bank-conflict cycles, not the read latency,
             // bound the taps (profiles/r04).  Same arithmetic, same order per pixel either way.
-            constexpr int NSL = 4 * K, PF = kResPF;
+            // 128-thread builds (small parts, e.g. C1's 247 of 72 quads: two waves, the taps one
+            // wave's dependency chain) issue the reads 4 slots ahead: C1 +3.9 % same-box; the
+            // 576-thread builds (nine waves keep the LDS busy) lose 4 % with it
+            // (profiles/r04/ab_pf_r4s_*.txt)
+            // (fp32: the fp16 build spills with it)
+            constexpr int NSL = 4 * K, PF = (NTC == 128 && kResPF == 0 && ES == 4) ? 4 : kResPF;
             float2 g01[NSL], g23[NSL];
             float4 akv[K + 1];
             float4 cref;  // the reference tap's own-quad cells (one-cell form; the four-corner
@@ -778,7 +783,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
             for (int s = 0; s < NSL; ++s) {
                 if (s + PF < NSL) issue(s + PF);
-                if constexpr (kResPF > 0) __builtin_amdgcn_sched_barrier(0);
+                if constexpr (PF > 0) __builtin_amdgcn_sched_barrier(0);
                 const int k = s >> 2, e = s & 3;
                 if (PF == 0) issue(s);
                 if (s == 4 * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
