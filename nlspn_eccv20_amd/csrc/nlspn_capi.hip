@@ -173,7 +173,7 @@ int prepare_step(StepReq &r, StepLaunch &L) {
 
 // A plan's launch record: enough to re-issue one kernel launch without a graph.
 struct LaunchRec {
-    const void *fn;  // null: a memset of zbytes at zptr (the resident kernel's progress words)
+    const void *fn;  // null: a memset of zbytes at zptr (unused since round 4: step 1 zeroes the sync words)
     dim3 grid, block;
     size_t lds;
     bool resident;
@@ -896,7 +896,7 @@ int nlspn_prop_step(int dtype, const void *p_in, const void *conf, const void *d
 
 size_t nlspn_workspace_bytes(int dtype, int B, int H, int W) {
     (void)dtype; (void)B; (void)H; (void)W;
-    return kSyncBytes;  // the resident kernel's progress words (the prologue needs no scratch)
+    return kSyncBytes;  // the resident kernel's sync words (the prologue needs no scratch)
 }
 
 int nlspn_propagate(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,

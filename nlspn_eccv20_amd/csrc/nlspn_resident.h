@@ -326,8 +326,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // Part numbering: logical index L = b * (gy*gx) + j, dealt to the XCDs in contiguous
     // runs (xcd_remap), so the parts of an image — and neighbouring parts — share an
     // XCD where the counts allow (C2: one image per XCD; C3: each image over four XCDs
-    // in bands of 32 parts; C1: bands of 32 parts).  Speed only: progress words are
-    // indexed by blockIdx, and a consumer maps the parts it reads back (xcd_unmap).
+    // in bands of 32 parts).  Speed only: the placement words are indexed by blockIdx, and
+    // a reader maps the parts of its image back (xcd_unmap).
     const int nparts = a.gy * a.gx, G = a.B * nparts;
     // (bid: blockIdx behind an opaque move, so that nothing derived from it is hoisted
     // out of the group loop and held in registers across the groups)

@@ -289,7 +289,7 @@ def _alloc_outputs(pred_init, K, T, with_off, with_conf):
         "aff": torch.empty((B, K + 1, H, W), **kw_),
         "offset": torch.empty((B, 2 * (K + 1), H, W), **kw_) if with_off else None,
         "confidence": torch.empty((B, 1, H, W), **kw_) if with_conf else None,
-        # progress words of the resident kernel (iterations 2..T in one launch)
+        # sync words of the resident kernel (abort word, per-part placement words)
         "workspace": torch.empty(_lib.get().nlspn_workspace_bytes(_dtype_code(pred_init), B, H, W) // 4,
                                  dtype=torch.int32, device=pred_init.device),
     }

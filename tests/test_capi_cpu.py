@@ -29,7 +29,7 @@ def test_library_exports_header_symbols():
 def test_abi_version_and_workspace():
     lib = _lib.get()
     assert lib.nlspn_abi_version() == 3
-    # resident kernel progress words (a 16-B multiple: one word per workgroup + abort word)
+    # resident kernel sync words (a 16-B multiple: one 128-B line per workgroup + the abort line)
     assert lib.nlspn_workspace_bytes(0, 8, 228, 304) == 513 * 128  # one 128-B sync line per resident part
     assert lib.nlspn_resident_config(0, 8, 228, 304, 3, 3, 18, 1, None, None, None) == 0  # no GPU here
     # backward: dL/df ping-pong + K planes of G + dL/dconf' + one dL/dgamma partial per 8x32 tile
