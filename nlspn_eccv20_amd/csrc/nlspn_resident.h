@@ -114,6 +114,9 @@ constexpr int kResPF = NLSPN_RES_PF;
 #ifndef NLSPN_RES_FMA
 #define NLSPN_RES_FMA 0  // timing experiment only: contracted bilinear (not the oracle's arithmetic)
 #endif
+#ifndef NLSPN_RES_SPIN_SLEEP
+#define NLSPN_RES_SPIN_SLEEP 1  // s_sleep between a staging spin's re-loads (A/B builds: 0, 2, 4)
+#endif
 #ifndef NLSPN_RES_WTRACE
 #define NLSPN_RES_WTRACE 0  // trace builds: per-wave stamps too (they cost the loop 16 B/lane of scratch)
 #endif
@@ -663,7 +666,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
                 unsigned spins = 0;
                 while (!fail && __builtin_amdgcn_ballot_w64(!ok) != 0) {
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(NLSPN_RES_SPIN_SLEEP);
                     if (!ok) {
                         ok = true;
 #pragma unroll
