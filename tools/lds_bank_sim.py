@@ -26,33 +26,29 @@ def res_shape(B, H, W, cus=256):
     W4 = W // 4
     Q = H * W4
     for Bg in range(min(B, cus), 0, -1):
-        for capped in (1, 0):
-            gcap = max(1, cus // 8) if capped else cus
-            if capped and cus // Bg <= gcap:
-                continue
-            gmax = min(min(cus // Bg, gcap), max(1, Q // 64))
-            best, res = 1e300, None
-            for g in range(gmax, max(1, gmax * 3 // 4) - 1, -1):
-                for gy in range(1, g + 1):
-                    if g % gy:
-                        continue
-                    gx = g // gy
-                    if gy > H or gx > W4:
-                        continue
-                    ph, pq = -(-H // gy), -(-W4 // gx)
-                    nq = ph * pq
-                    nt = -(-nq // 64) * 64
-                    if nt > 768:
-                        continue
-                    fb = (ph + 2 * RY) * (4 * (pq + 2 * RXQ) + 2 * PADX)
-                    if win_cells(nt) < fb:
-                        continue
-                    rim = ((ph + 18) * (4.0 * pq + 18) - 4.0 * nq) / 4.0
-                    cost = nq + 0.2 * rim
-                    if cost < best:
-                        best, res = cost, (Bg, gy, gx, nt)
-            if res:
-                return res
+        gmax = min(cus // Bg, max(1, Q // 64))
+        best, res = 1e300, None
+        for g in range(gmax, max(1, gmax * 3 // 4) - 1, -1):
+            for gy in range(1, g + 1):
+                if g % gy:
+                    continue
+                gx = g // gy
+                if gy > H or gx > W4:
+                    continue
+                ph, pq = -(-H // gy), -(-W4 // gx)
+                nq = ph * pq
+                nt = -(-nq // 64) * 64
+                if nt > 768:
+                    continue
+                fb = (ph + 2 * RY) * (4 * (pq + 2 * RXQ) + 2 * PADX)
+                if win_cells(nt) < fb:
+                    continue
+                rim = ((ph + 18) * (4.0 * pq + 18) - 4.0 * nq) / 4.0
+                cost = nq + 0.2 * rim
+                if cost < best:
+                    best, res = cost, (Bg, gy, gx, nt)
+        if res:
+            return res
     raise ValueError("no shape")
 
 
