@@ -286,7 +286,8 @@ bool stream_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-bool res_guard_off() {  // A/B measurement only: NLSPN_RES_GUARD=0
+bool res_guard_off() {  // A/B measurement only, experiments build: NLSPN_RES_GUARD=0
+    if (!kExperiments) return false;
     static const bool off = [] { const char *e = getenv("NLSPN_RES_GUARD"); return e && e[0] == '0'; }();
     return off;
 }
@@ -328,6 +329,7 @@ struct ResPlan {
     unsigned block = 0;
     size_t lds = 0, sync_bytes = 0;
     int ngroups = 0;
+    int err = 0;  // nonzero: the plan was refused with an error (not a fallback), see nlspn_last_error
     unsigned grid[kResMaxGroups] = {};
     ResArgs a[kResMaxGroups];
 };
@@ -441,7 +443,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     P.ngroups = ng;
     DevState *ds = dev_state();
     unsigned dbg = 0;
-    if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
+    if (kExperiments)
+        if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
     const int K = 8;
     // Same-XCD hand-offs in the XCD's L2 (kResL2, nlspn_resident.h): possible where every
     // image plane of every iteration starts and ends on a 128-B line (no line is shared
@@ -472,6 +475,16 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // per group.
     const char *menv = getenv("NLSPN_RES_MERGE");
     const int nfull = B / S.Bg;
+    if (dbg & 8u) {  // trace stamps (experiments build) go into pred: each launch's part must hold them
+        const long long per = (long long)T * (kResWTrace ? 29 : 5) * 8;
+        for (int k = 0; k < ng; ++k)
+            if ((long long)(B - (long long)k * S.Bg) * HW * (long long)es < (long long)P.grid[k] * per) {
+                P.err = fail(NLSPN_EINVAL, "resident trace (NLSPN_RES_DBG=8): pred holds %lld bytes from image group %d, "
+                             "the stamps need %lld", (long long)(B - (long long)k * S.Bg) * HW * (long long)es, k,
+                             (long long)P.grid[k] * per);
+                return false;
+            }
+    }
     if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
         P.a[0].ngroups = nfull;
         // the group-loop build for the merged launch; a partial last group keeps the other
@@ -637,6 +650,7 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
     ResPlan P;
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
                                    pred, workspace, B, H, W, kh, kw, T, flags, P);
+    if (P.err) return P.err;
     if (res) {  // step 1 zeroes the resident kernel's sync words and poisons plane 1 (its hand-off)
         r1.a.zero_words = P.a[0].sync;
         r1.a.nzero = (int)(P.sync_bytes / 4);
@@ -695,7 +709,8 @@ int nlspn_s2d_pyramid(int dtype, const void *dep, const float *w1, const float *
     if (!dep || !w1 || !b1 || !w2 || !b2 || !out) return fail(NLSPN_EINVAL, "null required pointer");
     S2DArgs a{static_cast<const float *>(dep), w1, b1, w2, b2, static_cast<float *>(out), static_cast<float *>(pyr),
               B, H, W, (W + kS2DTW - 1) / kS2DTW, (H + kS2DTH - 1) / kS2DTH, 0u};
-    if (const char *d = getenv("NLSPN_S2D_DBG")) a.dbg = (unsigned)atoi(d);
+    if (kExperiments)
+        if (const char *d = getenv("NLSPN_S2D_DBG")) a.dbg = (unsigned)atoi(d);
     const long long grid = (long long)B * a.tiles_x * a.tiles_y;
     if (grid > 0x7fffffffLL) return fail(NLSPN_EINVAL, "input too large");
     void *args[] = {&a};
@@ -759,7 +774,7 @@ static int launch_heads(HeadsArgs &a, void *stream) {
     if (a.aff_out)  // the fused propagation prologue (nout = 24: MB = 1)
         fn = vec ? reinterpret_cast<const void *>(&heads_kernel<1, true, 0, true>)
                  : reinterpret_cast<const void *>(&heads_kernel<1, false, 0, true>);
-    else if (vec && head_mb(nout) == 1 && (a.dbg & 3u)) {  // ablation kernels (timing only)
+    else if (kExperiments && vec && head_mb(nout) == 1 && (a.dbg & 3u)) {  // ablation kernels (timing only)
         const void *abl[3] = {reinterpret_cast<const void *>(&heads_kernel<1, true, 1>),
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 2>),
                               reinterpret_cast<const void *>(&heads_kernel<1, true, 3>)};
@@ -789,7 +804,8 @@ int nlspn_head_epilogue(int dtype, const void *fe1, const void *fd_oa, const voi
                 static_cast<float *>(pred_init), static_cast<float *>(conf), B, C, H, W, nout,
                 (W + kHdTW - 1) / kHdTW, (H + kHdTH - 1) / kHdTH, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                 0u, 0u};
-    if (const char *d = getenv("NLSPN_HEADS_DBG")) a.dbg = (unsigned)atoi(d);
+    if (kExperiments)
+        if (const char *d = getenv("NLSPN_HEADS_DBG")) a.dbg = (unsigned)atoi(d);
     return launch_heads(a, stream);
 }
 
@@ -841,6 +857,7 @@ int nlspn_propagate_normalized(int dtype, const void *p0, const void *dep, const
     ResPlan P;
     const bool res = plan_resident(dtype, conf_eff, dep, aff_norm, off_ins, 2LL * (K + 1) * HW, pred_inter, pred,
                                    workspace, B, H, W, kh, kw, T, flags | kResOffInserted, P);
+    if (P.err) return P.err;
     StepArgs a1 = r.a;
     if (res) {  // iteration 1 zeroes the resident kernel's sync words and poisons plane 1
         a1.zero_words = P.a[0].sync;

@@ -9,6 +9,17 @@ namespace nlspn {
 
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin (b, b+8 share one)
 
+// Experiment switches (the NLSPN_RES_DBG / NLSPN_S2D_DBG / NLSPN_HEADS_DBG ablation bits,
+// which make results wrong on purpose, and NLSPN_RES_GUARD=0) exist only in the
+// experiments build (make exp: lib/exp/libnlspn_hip_exp.so, loaded through
+// NLSPN_LIB_PATH for A/B runs and the abort-path tests).  In the product library the
+// environment is not read for them and every dbg branch folds away.
+#ifndef NLSPN_EXPERIMENTS
+#define NLSPN_EXPERIMENTS 0
+#endif
+constexpr bool kExperiments = NLSPN_EXPERIMENTS != 0;
+__host__ __device__ constexpr unsigned exp_dbg(unsigned d) { return kExperiments ? d : 0u; }
+
 // Element load/store with fp32 math regardless of storage type.
 template <typename T> __device__ __forceinline__ float ld(const T *p);
 template <> __device__ __forceinline__ float ld<float>(const float *p) { return *p; }

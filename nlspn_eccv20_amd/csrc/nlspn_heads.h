@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(kHdNT) __attribute__((amdgpu_waves_per_eu(2, 2
     load_round(0);
     for (int r = 0; r < nr; ++r) {
         __syncthreads();  // the previous round's LDS reads are done
-        if (!(a.dbg & 4u)) {
+        if (!(exp_dbg(a.dbg) & 4u)) {
             xm.store(XL, tid);
             xv.store(XV, tid);
 #pragma unroll

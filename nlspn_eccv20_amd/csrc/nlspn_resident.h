@@ -81,9 +81,12 @@ struct ResArgs {
     int win_cells;      // LDS cells per copy of the f window: res_win_cells(blockDim.x)
     unsigned epoch;     // tag base of this launch's XCC-id words (k * (T + 1) for image group k)
     unsigned flags;
-    unsigned dbg;       // experiments only (NLSPN_RES_DBG): 1 no spin on staged cells, 2 no staging,
-                        // 4 no taps, 8 trace: s_memrealtime stamps per part and iteration into `pred`
-                        // (then invalid), 32 part 0 aborts at its first staging (tests of the error path)
+    unsigned dbg;       // experiments build only (NLSPN_RES_DBG, exp_dbg; 0 and folded away in the
+                        // product library): 1 no spin on staged cells, 2 no staging, 4 no taps,
+                        // 8 trace: s_memrealtime stamps per part and iteration into `pred` (then
+                        // invalid; the host checks it is large enough), 32 part 0 aborts at its first
+                        // staging (tests of the error path), 64 no general path (wrong results for
+                        // taps outside the window: tests that it is taken)
     // image groups this launch runs in turn (0 or 1: one).  Group g is images
     // g*B .. g*B + B - 1 from the base pointers above: a part starts group g + 1 as soon
     // as it has stored its last iteration of group g, with no launch boundary between the
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (h_im, w_im) = (y - PH + i + dh, x - PW + j + dw), the reference's own
     // expression (.cuh:178-179), so the geometry below starts from them.
     // trace (dbg 8): row t = 0 of this part holds the setup stamps
-    unsigned long long *trace0 = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
+    unsigned long long *trace0 = (exp_dbg(a.dbg) & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                    (size_t)blockIdx.x * a.T * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
     // trace: per wave and iteration two more stamps (taps + stores issued, stores drained)
@@ -598,7 +601,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     int t_abort = 0;
     for (int t = 1; t < a.T; ++t) {
-        unsigned long long *trace = (a.dbg & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
+        unsigned long long *trace = (exp_dbg(a.dbg) & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
                                                        ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
         const rsrc_t rp = make_rsrc(p_all + (size_t)(t - 1) * a.tstride + b * HW);
@@ -633,11 +636,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // plain loads (invariant).  After a launch's first iteration the own quads are in the
         // window already (written back below), so only the other parts' quads are loaded.
         const bool rim = t > 1;
-        const bool spin = rim && !(a.dbg & 1u);
+        const bool spin = rim && !(exp_dbg(a.dbg) & 1u);
         // the staging index (= tid) rebuilt per iteration from the wave's base (an SGPR) and
         // the lane id, so no VGPR holds it across the loop (it was spilled and reloaded)
         const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        const int nsq_it = (a.dbg & 2u) ? 0 : (rim ? nrest : nall);
+        const int nsq_it = (exp_dbg(a.dbg) & 2u) ? 0 : (rim ? nrest : nall);
         bool nonfin = false;  // this thread staged a non-finite f
         for (int base = tb; base < nsq_it; base += SMAX * NT) {
             float sv[SMAX][4], cv[SMAX][4];
@@ -663,7 +666,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
             if (spin) {  // this wave's lanes re-load the quads still poisoned (a bounded spin)
-                bool fail = (a.dbg & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
+                bool fail = (exp_dbg(a.dbg) & 32u) && L == 0;  // test hook: part 0 of image 0 aborts
                 unsigned spins = 0;
                 while (!fail && __builtin_amdgcn_ballot_w64(!ok) != 0) {
                     __builtin_amdgcn_s_sleep(NLSPN_RES_SPIN_SLEEP);
@@ -732,7 +735,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
         }
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
-        if (active && !(a.dbg & 4u)) {
+        if (active && !(exp_dbg(a.dbg) & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             // branch-free path: every tap from the LDS window (invalid taps read zeros), in
             // 32 tap-pixel slots s = 4k + e.  kResPF > 0 (A/B builds) issues slot s + PF's two
@@ -818,7 +821,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // cells every iteration, re-loaded until not the poison, as the staging's).  It
             // re-reads its offsets from global memory and runs a rolled tap loop, so it
             // shares no registers with the branch-free path (no spills around it).
-            if (kResGeneralPath && wave_fb && has_fb) {
+            // A corner spin that times out (or sees another part's abort: polled every 16
+            // spins) raises the abort like the staging spin's, and the lane stops spinning on
+            // later corners (gp_fail); the poison then reaches the sum as a NaN, and the abort
+            // fill below the loop covers the later planes.
+            bool gp_fail = false;
+            if (kResGeneralPath && wave_fb && has_fb && !(exp_dbg(a.dbg) & 64u)) {
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
                 // the own quad's row and first column, recomputed from its byte offset (not
                 // live across the loop)
@@ -865,7 +873,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                         for (unsigned sp = 0;; ++sp) {  // per lane, bounded
                                             bool rdy;
                                             pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
-                                            if (rdy || t == 1 || (a.dbg & 1u) || sp > kResSpinLimit) break;
+                                            if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
+                                            if (sp > kResSpinLimit ||
+                                                ((sp & 15u) == 15u &&
+                                                 __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+                                                gp_fail = true;
+                                                break;
+                                            }
                                             __builtin_amdgcn_s_sleep(1);
                                         }
                                         c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
@@ -878,6 +892,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     }
                     acc[e] = s;
                 }
+            }
+            if (gp_fail) {  // (rare lanes; every writer stores 1)
+                ctl[0] = 1;
+                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             // the reference tap in the reference's four-corner form (.cuh:37-52: the integer
             // point's weights are exactly (1, 0, 0, 0)) differs from the one-cell form used
@@ -913,7 +932,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             else ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
 #pragma unroll
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
-            if (t == a.T - 1 && !(a.dbg & 8u))
+            if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
                 ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
         }
         if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
@@ -924,7 +943,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (tid == 0) ctl[6 + (t & 1)] = 0;  // iteration t's flag, next used by iteration t + 2
         // ---- the own quad's f_t = p_t * conf' straight into the window, as the next
         // staging would load it
-        if (t < a.T - 1 && active && !(a.dbg & 2u)) {
+        if (t < a.T - 1 && active && !(exp_dbg(a.dbg) & 2u)) {
             const float4 cw = akl[K + 1];
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
             if (has_conf) {

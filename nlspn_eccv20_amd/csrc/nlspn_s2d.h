@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) s2d_pyramid_kernel(S2DArgs a) {
 
     // ---- pass 1: horizontal, every window row x tile column.  Out-of-image cells
     // are the pools' -inf padding: skipped (a row outside the image: +inf / -inf).
-    for (int i = threadIdx.x; i < ((a.dbg & 2u) ? 0 : WH * TW); i += 256) {
+    for (int i = threadIdx.x; i < ((exp_dbg(a.dbg) & 2u) ? 0 : WH * TW); i += 256) {
         const int r = i / TW, c = i % TW, gy = y0 - R + r, x = x0 + c;
         float mn = INF, mx = -INF;
         if (gy >= 0 && gy < H && x < W) {
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) s2d_pyramid_kernel(S2DArgs a) {
                 m = r <= 4 ? fminf(m, col[-d * TW]) : fmaxf(m, col[-d * TW]);
                 m = r <= 4 ? fminf(m, col[d * TW]) : fmaxf(m, col[d * TW]);
             }
-            pyr[p][r - 1] = (a.dbg & 1u) ? 0.f : (r <= 4 ? (m == 999.0f ? 0.0f : m) : m);
+            pyr[p][r - 1] = (exp_dbg(a.dbg) & 1u) ? 0.f : (r <= 4 ? (m == 999.0f ? 0.0f : m) : m);
         }
     }
     // pool_convs (:455): two 1x1 conv + bias + ReLU, input channels in index order
@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(256) s2d_pyramid_kernel(S2DArgs a) {
     const long long px = (long long)y * W + x;
     float *out = a.out + (long long)b * 17 * HW + px;
     auto put = [&](float *dst, const float (&v)[4]) {
-        if (a.dbg & 4u) {
+        if (exp_dbg(a.dbg) & 4u) {
             if (v[0] == 12345.f) a.out[0] = v[1];  // keep the math alive
             return;
         }

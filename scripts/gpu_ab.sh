@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of library builds / env toggles: C2 bench value, alternated rounds.
 # usage: scripts/gpu_ab.sh NAME=LIBPATH_OR_-[:ENV=VAL] ...   ("-" = the in-tree build)
-# e.g.   scripts/gpu_ab.sh cur=- r01=nlspn_eccv20_amd/lib/ab/libnlspn_r01.so noguard=-:NLSPN_RES_GUARD=0
+# e.g.   scripts/gpu_ab.sh cur=- r01=nlspn_eccv20_amd/lib/ab/libnlspn_r01.so noguard=nlspn_eccv20_amd/lib/exp/libnlspn_hip_exp.so:NLSPN_RES_GUARD=0
 set -o pipefail
 O=gpurun_out/ab; mkdir -p $O
 CFG=${AB_CONFIG:-nyu}

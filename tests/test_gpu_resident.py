@@ -216,17 +216,21 @@ def test_resident_replays_stable_and_no_abort():
         plan.close()
 
 
-@pytest.mark.parametrize("B,H,W,l2,dtype", [
-    (8, 228, 304, "1", torch.float32), (8, 228, 304, "0", torch.float32), (4, 240, 1216, "1", torch.float32),
-    (1, 228, 304, "1", torch.float32), (8, 228, 304, "1", torch.float16)])
-def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype):
+@pytest.mark.parametrize("B,H,W,l2,dtype,sigma", [
+    (8, 228, 304, "1", torch.float32, 3.0), (8, 228, 304, "0", torch.float32, 3.0),
+    (4, 240, 1216, "1", torch.float32, 3.0), (1, 228, 304, "1", torch.float32, 3.0),
+    (8, 228, 304, "1", torch.float16, 3.0),
+    (4, 96, 128, "1", torch.float32, 12.0), (2, 120, 2048, "1", torch.float32, 12.0)])
+def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype, sigma):
     """Replays over in-place refilled inputs that alternate between two data sets: every
     plane a hand-off reads was last written with the OTHER set's values, so a consumer that
     took a previous call's cell instead of waiting out the poison (nlspn_resident.h) changes
     the result.  Long-range offsets (sigma 3), L2-kept and write-through hand-offs, the
-    two-group merged launch (KITTI B=4), one image over 32 parts, fp16 storage."""
-    ia, _ = _inputs(B, H, W, sigma=3.0, seed=31, dtype=dtype)
-    ib, _ = _inputs(B, H, W, sigma=3.0, seed=32, dtype=dtype)
+    two-group merged launch (KITTI B=4), one image over 247 parts, fp16 storage; and two
+    fixed-halo shapes at sigma 12 whose far taps take the general path (global re-reads of
+    the same cells every iteration; test_general_path_taken_at_fixed_halo_shapes)."""
+    ia, _ = _inputs(B, H, W, sigma=sigma, seed=31, dtype=dtype)
+    ib, _ = _inputs(B, H, W, sigma=sigma, seed=32, dtype=dtype)
     with _env("0"):
         ra = propagate(*ia, prop_time=18)["pred_inter_tensor"].clone()
         rb = propagate(*ib, prop_time=18)["pred_inter_tensor"].clone()
@@ -318,35 +322,6 @@ def test_merged_groups_and_partial_group_bit_exact(dtype):
     _lib.check_resident()
 
 
-def test_merged_launch_abort_raises_and_poisons():
-    """An abort inside a merged (two-group) launch: RuntimeError, and NaN — not stale or
-    plausible depths — in the planes the aborted part never wrote, for every group."""
-    inp, _ = _inputs(4, 240, 1216, seed=12)
-    old = os.environ.get("NLSPN_RES_DBG")
-    os.environ["NLSPN_RES_DBG"] = "32"
-    try:
-        with _env("1"):
-            plan = PropagationPlan(*inp, prop_time=18)
-        o = plan.replay()
-        with pytest.raises(RuntimeError, match="aborted"):
-            plan.check()
-        p = o["pred_inter_tensor"]
-        assert torch.isnan(p[1:, 0]).any()  # group 0: the aborting part's own image
-        assert torch.isnan(p[1:, 2]).any() and torch.isnan(o["pred"][2]).any()  # its quads of group 1
-        plan.close()
-    finally:
-        if old is None:
-            os.environ.pop("NLSPN_RES_DBG", None)
-        else:
-            os.environ["NLSPN_RES_DBG"] = old
-    _lib.check_resident()
-    with _env("1"):
-        o = propagate(*inp, prop_time=18)
-    torch.cuda.synchronize()
-    _lib.check_resident()
-    assert not torch.isnan(o["pred"]).any()
-
-
 def test_two_plans_on_two_streams_bit_exact():
     """Two resident plans replayed concurrently on two streams of one device: the
     library serialises resident launches across streams (co-residency), so every
@@ -378,32 +353,48 @@ def test_two_plans_on_two_streams_bit_exact():
         pb.close()
 
 
-def test_aborted_launch_raises_and_poisons():
-    """A resident launch that aborts (forced here: NLSPN_RES_DBG=32 makes part 0 abort) sets
-    the device's sticky status: the next call / check() raises RuntimeError, and the
-    planes the aborted parts never wrote hold NaN, not plausible depths."""
+def _exp_case(*args):
+    """Runs a case of tests/_exp_cases.py in a child process on the EXPERIMENTS build of the
+    library (the NLSPN_RES_DBG switches exist only there; the product library ignores them)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "nlspn_eccv20_amd", "lib", "exp", "libnlspn_hip_exp.so")
+    assert os.path.exists(lib), "experiments build missing: make -C nlspn_eccv20_amd/csrc exp"
+    env = dict(os.environ, NLSPN_LIB_PATH=lib)
+    env.pop("NLSPN_RES_DBG", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "tests", "_exp_cases.py")] + [str(a) for a in args],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0 and "ok" in out.stdout, (out.stdout[-2000:], out.stderr[-3000:])
+
+
+@pytest.mark.parametrize("B,H,W,seed", [(8, 228, 304, 5), (4, 240, 1216, 12)])
+def test_aborted_launch_raises_and_poisons(B, H, W, seed):
+    """A resident launch that aborts (experiments build, NLSPN_RES_DBG=32: part 0 aborts)
+    sets the device's sticky status: check() raises RuntimeError and the planes the
+    aborted parts never wrote hold NaN, not plausible depths — in a one-group launch (C2)
+    and in a merged two-group launch (KITTI B=4), every group.  The next call runs clean."""
+    _exp_case("abort", B, H, W, seed)
+
+
+def test_product_library_ignores_experiment_switches():
+    """The product library reads no NLSPN_RES_DBG: with the abort bit set in the
+    environment a propagation is bit-exact and nothing aborts."""
     inp, _ = _inputs(8, 228, 304, seed=5)
-    old = os.environ.get("NLSPN_RES_DBG")
-    os.environ["NLSPN_RES_DBG"] = "32"
-    try:
-        with _env("1"):
-            plan = PropagationPlan(*inp, prop_time=18)
-        o = plan.replay()
-        with pytest.raises(RuntimeError, match="aborted"):
-            plan.check()
-        assert torch.isnan(o["pred_inter_tensor"][1:]).any()
-        plan.close()
-    finally:
-        if old is None:
-            os.environ.pop("NLSPN_RES_DBG", None)
-        else:
-            os.environ["NLSPN_RES_DBG"] = old
-    _lib.check_resident()  # the sticky word was cleared by the raise
     with _env("1"):
-        o = propagate(*inp, prop_time=18)
+        ref = propagate(*inp, prop_time=18)["pred_inter_tensor"].clone()
+        with _env("32", "NLSPN_RES_DBG"):
+            o = propagate(*inp, prop_time=18)["pred_inter_tensor"]
     torch.cuda.synchronize()
     _lib.check_resident()
-    assert not torch.isnan(o["pred"]).any()
+    assert torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("B,H,W,sigma", [(4, 96, 128, 12.0), (2, 120, 2048, 12.0)])
+def test_general_path_taken_at_fixed_halo_shapes(B, H, W, sigma):
+    """The fixed-halo shapes of the alternating-input test do take the general path (its
+    results change when the experiments build switches that path off)."""
+    _exp_case("general_path", B, H, W, sigma)
 
 
 def test_plan_first_in_fresh_process():

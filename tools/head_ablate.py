@@ -9,6 +9,9 @@ import torch
 import torch.nn as nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the NLSPN_*_DBG switches exist only in the experiments build (make -C nlspn_eccv20_amd/csrc exp)
+os.environ.setdefault("NLSPN_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "nlspn_eccv20_amd", "lib", "exp", "libnlspn_hip_exp.so"))
 from nlspn_eccv20_amd.heads import HeadWeights, head_epilogue  # noqa: E402
 from tools.head_prof import timed  # noqa: E402
 

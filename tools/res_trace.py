@@ -14,6 +14,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the NLSPN_*_DBG switches exist only in the experiments build (make -C nlspn_eccv20_amd/csrc exp)
+os.environ.setdefault("NLSPN_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "nlspn_eccv20_amd", "lib", "exp", "libnlspn_hip_exp.so"))
 from nlspn_eccv20_amd import _lib  # noqa: E402
 from nlspn_eccv20_amd.propagation import _alloc_outputs, _propagate_args, _stream  # noqa: E402
 from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
