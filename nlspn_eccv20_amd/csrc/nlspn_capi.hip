@@ -32,6 +32,8 @@ namespace nlspn {
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
 NLSPN_RES_EXTERN(float)
 NLSPN_RES_EXTERN(__half)
+extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>(ResArgs);
 // defined in nlspn_kern_heads.hip
 #define NLSPN_HD_EXTERN(MB)                                            \
     extern template __global__ void heads_kernel<MB, true>(HeadsArgs); \
@@ -335,10 +337,14 @@ struct ResPlan {
 };
 
 template <typename T>
-const void *res_fn(long long nt, bool groups, bool pitch_ok) {
+const void *res_fn(long long nt, bool groups, bool pitch_ok, bool tail) {
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
+    if (tail) {  // the eight-wave build (fp32 only; the planner checked its pitch)
+        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>);
+        return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>);
+    }
     if (groups)
         return nt == 576 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>)
                          : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>);
@@ -398,7 +404,7 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
 // Fills P and returns true when the resident kernel applies (iterations 2..T).
 bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
-                   int kw, int T, unsigned flags, ResPlan &P) {
+                   int kw, int T, unsigned flags, ResPlan &P, void *off_out = nullptr) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
@@ -427,16 +433,31 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (ng > kResMaxGroups) return false;
     const unsigned G = (unsigned)(S.Bg * S.gy * S.gx);
     if ((size_t)(G + 1) * 4 * kResLine > kSyncBytes) return false;
-    // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
-    // res_win_cells, may need less: the request is padded)
-    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + 16 * kResAS * (size_t)S.nt,
-                                        80 * 1024 + 16);
-    if (lds > (size_t)kResLds) return false;
     // the fixed-halo window of the largest part within the 576-thread builds' pitch / cells
     const int php = (H + S.gy - 1) / S.gy, pqp = (W / 4 + S.gx - 1) / S.gx;
     const bool pitch_ok = 4 * (pqp + 2 * kResRXQ) + 2 * kResPadX <= res_pitch(576) &&
                           (php + 2 * kResRY) * res_pitch(576) <= res_win_cells(576);
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false, pitch_ok) : res_fn<__half>(S.nt, false, pitch_ok);
+    // The eight-wave build (nlspn_resident.h kResTailNT; fp32): parts of 449..576 quads
+    // (C2 541.5, C3 570), whose 512 threads own a quad each and the rest as tail pixels;
+    // its window has the same 128-cell pitch.  NLSPN_RES_TAIL=0 / 1 (A/B) forces the 576-thread
+    // build / this one there (bit-identical); unset: kResTailDefault.
+    const char *tenv = getenv("NLSPN_RES_TAIL");
+    const bool tail_on = tenv && (tenv[0] == '0' || tenv[0] == '1') ? tenv[0] == '1' : kResTailDefault;
+    const bool tail = dtype == NLSPN_DTYPE_F32 && tail_on && php * pqp > kResTailNT - 64 &&
+                      php * pqp <= kResTailNT + kResTailQuads &&
+                      4 * (pqp + 2 * kResRXQ) + 2 * kResPadX <= res_pitch(kResTailNT) &&
+                      (php + 2 * kResRY) * res_pitch(kResTailNT) <= kResTailWC;
+    if (tail) {
+        S.nt = kResTailNT;
+        S.win_cells = kResTailWC;
+    }
+    // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
+    // res_win_cells, may need less: the request is padded); the eight-wave build keeps
+    // conf' / dep planes and the tail pixels' planes instead of per-thread rows
+    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : 16 * kResAS * (size_t)S.nt),
+                                        80 * 1024 + 16);
+    if (lds > (size_t)kResLds) return false;
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false, pitch_ok, tail) : res_fn<__half>(S.nt, false, pitch_ok, false);
     P.block = (unsigned)S.nt;
     P.lds = lds;
     P.sync_bytes = (size_t)(G + 1) * 4 * kResLine;
@@ -453,6 +474,9 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const char *l2env = getenv("NLSPN_RES_L2");
     const bool l2ok = !(l2env && l2env[0] == '0') && ((long long)HW * (long long)es) % 128 == 0 &&
                       aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
+    const char *cenv = getenv("NLSPN_RES_OFFCOPY");
+    const bool copy_off = off_out && !(flags & kResOffInserted) && !(cenv && cenv[0] == '0') &&
+                          aligned(off_out, vb);
     for (int k = 0; k < ng; ++k) {
         const long long b0 = (long long)k * S.Bg;
         const int Bk = (int)std::min<long long>(S.Bg, B - b0);
@@ -467,6 +491,9 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          static_cast<unsigned *>(workspace), ds ? ds->dev_status : nullptr, off_bs, (long long)B * HW,
                          Bk, H, W, T, S.gy, S.gx, S.win_cells, (unsigned)(k * (T + 1)),
                          flags | (l2ok ? kResL2 : 0u), dbg};
+        // the output dict's inserted offsets copied by the resident loop (ResArgs::off_out)
+        // instead of step 1; NLSPN_RES_OFFCOPY=0 (A/B) leaves them to step 1
+        if (copy_off) P.a[k].off_out = const_cast<void *>(at(off_out, b0 * 2 * (K + 1) * HW));
     }
     // The full image groups run in turn inside ONE launch (ResArgs::ngroups): no launch
     // boundary between them, so a part sets up its next group while others finish the
@@ -488,7 +515,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
         P.a[0].ngroups = nfull;
         // the group-loop build for the merged launch; a partial last group keeps the other
-        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true, pitch_ok) : res_fn<__half>(S.nt, true, pitch_ok);
+        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true, pitch_ok, tail) : res_fn<__half>(S.nt, true, pitch_ok, false);
         int n = 1;
         if (ng > nfull) {  // the partial group, launched after the merged one
             P.a[1] = P.a[ng - 1];
@@ -649,8 +676,9 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
     if (resident) *resident = 0;
     ResPlan P;
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
-                                   pred, workspace, B, H, W, kh, kw, T, flags, P);
+                                   pred, workspace, B, H, W, kh, kw, T, flags, P, off_out);
     if (P.err) return P.err;
+    if (res && P.a[0].off_out) r1.a.off_out = nullptr;  // the resident loop copies the offsets
     if (res) {  // step 1 zeroes the resident kernel's sync words and poisons plane 1 (its hand-off)
         r1.a.zero_words = P.a[0].sync;
         r1.a.nzero = (int)(P.sync_bytes / 4);

@@ -17,4 +17,8 @@ namespace nlspn {
     template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
 NLSPN_RES_INST(float)
 NLSPN_RES_INST(__half)
+// the eight-wave build (kResTailNT: affinities in VGPRs, tail pixels; fp32), launch bound 512
+// (two waves per SIMD: 256 VGPRs per lane)
+template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>(ResArgs);
+template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>(ResArgs);
 }  // namespace nlspn

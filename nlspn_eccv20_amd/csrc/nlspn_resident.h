@@ -92,6 +92,11 @@ struct ResArgs {
     // as it has stored its last iteration of group g, with no launch boundary between the
     // groups.
     int ngroups;
+    // The output dict's inserted offsets (nlspnmodel.py:324 `offset`: 2(K+1) planes per item,
+    // contiguous), or null (step 1 writes them): this launch copies them from the raw `off`
+    // planes, one output plane per iteration, so the copy rides the latency-bound loop instead
+    // of step 1's HBM-bound pass (raw offset layout only).
+    void *off_out;
 };
 
 typedef const __attribute__((address_space(4))) ResArgs ResArgsK;  // the kernarg segment's ResArgs
@@ -101,6 +106,10 @@ constexpr int kResMaxNT = 768;                  // launch bound (threads per par
 #define NLSPN_RES_SMAX 1
 #endif
 constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per round
+#ifndef NLSPN_RES_TAIL_SMAX
+#define NLSPN_RES_TAIL_SMAX 1
+#endif
+constexpr int kResTailSMax = NLSPN_RES_TAIL_SMAX;  // the same, eight-wave build (A/B builds: 2, 3)
 #ifndef NLSPN_RES_PF
 #define NLSPN_RES_PF 0
 #endif
@@ -130,6 +139,20 @@ constexpr int kResCtl = 8;                       // LDS control words ahead of t
 constexpr int kResAS = 11;                       // float4 per thread: K = 8 affinities, 1 - sum, conf', dep
 constexpr int kResLds = 160 * 1024;              // LDS per CU
 
+// The eight-wave build (threads 512, fp32; round 5): two waves per SIMD instead of nine
+// waves over four SIMDs (one of which held three, the taps' VALU bound), the affinities,
+// the reference-tap weight, conf' and dep of the thread's quad in VGPRs instead of LDS rows
+// (256 VGPRs per lane at two waves per SIMD), and the part's quads beyond the 512 the threads
+// own as quads split into single TAIL pixels, one per lane of waves 4..7 (one wave of each
+// SIMD): a part of up to 576 quads (C2 541.5, C3 570) costs every SIMD at most 4 + 5 pixel-
+// slots of taps per iteration where the nine-wave build cost one SIMD 3 x 4.
+constexpr int kResTailNT = 512;
+constexpr bool kResTailDefault = false;          // (measured slower so far: opt-in, NLSPN_RES_TAIL=1)
+constexpr int kResTailQuads = 64;                // tail capacity: 4 waves x 64 lanes = 256 pixels
+// its LDS after the window: conf' and dep of every thread's quad (two float4 planes of NT,
+// structure of arrays: conflict-free), then the tail pixels' K + 3 values (planes of 256)
+__host__ __device__ constexpr int res_tail_rows_bytes() { return 16 * 2 * kResTailNT + 4 * (8 + 3) * 256; }
+
 // LDS cells per copy of the f window for nt threads: what the per-thread rows leave,
 // a multiple of 4 (16-B aligned copies), both copies addressable by 16-bit indices.
 __host__ __device__ constexpr int res_win_cells(int nt) {
@@ -137,12 +160,17 @@ __host__ __device__ constexpr int res_win_cells(int nt) {
                ? ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4)
                : 32764;
 }
+// The eight-wave build keeps no per-thread rows: its two copies stay within 16-bit byte
+// addresses (4 * (kResCtl + 2 * 8,184) < 65,536).
+constexpr int kResTailWC = 8184;
 
 // the compile-time window pitch of a fixed-thread-count build (0: the pitch is the window's
 // width, a run-time value): 128 cells for 576 threads, whose two window copies span
-// 2 * 7,804 cells = 62.4 KB of byte addresses (below 64 KB: 16-bit)
-__host__ __device__ constexpr int res_pitch(int ntc) { return ntc == 576 ? 128 : 0; }
+// 2 * 7,804 cells = 62.4 KB of byte addresses (below 64 KB: 16-bit), and for the eight-wave
+// build (2 * 8,184 cells)
+__host__ __device__ constexpr int res_pitch(int ntc) { return ntc == 576 || ntc == kResTailNT ? 128 : 0; }
 static_assert(4 * (kResCtl + 2 * res_win_cells(576)) < 65536, "576-thread window byte addresses need 16 bits");
+static_assert(4 * (kResCtl + 2 * kResTailWC) < 65536, "eight-wave window byte addresses need 16 bits");
 
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
 #ifndef NLSPN_RES_NOGP
@@ -240,6 +268,18 @@ template <> struct ResVec<float> {
         const u32x4 q = {p, p, p, p};
         __builtin_amdgcn_raw_buffer_store_b128(q, r, vo, 0u, AUX);
     }
+    // one element (the eight-wave build's tail pixels: consecutive lanes, consecutive
+    // pixels, so a wave's dword stores coalesce)
+    template <unsigned AUX>
+    static __device__ __forceinline__ void store1(rsrc_t r, unsigned vo, unsigned so, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, AUX);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void poison1(rsrc_t r, unsigned vo) {
+        unsigned p = kResPoison32;
+        asm volatile("" : "+v"(p));
+        __builtin_amdgcn_raw_buffer_store_b32(p, r, vo, 0u, AUX);
+    }
 };
 template <> struct ResVec<__half> {
     template <unsigned AUX>
@@ -283,11 +323,21 @@ template <> struct ResVec<__half> {
         const u32x2 q = {w, w};
         __builtin_amdgcn_raw_buffer_store_b64(q, r, vo, 0u, AUX);
     }
+    // (the tail pixels are an fp32-only build: these exist for the shared kernel text)
+    template <unsigned AUX>
+    static __device__ __forceinline__ void store1(rsrc_t r, unsigned vo, unsigned so, float v) {
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v), r, vo, so, AUX);
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void poison1(rsrc_t r, unsigned vo) {
+        __builtin_amdgcn_raw_buffer_store_b16(kResPoison16, r, vo, 0u, AUX);
+    }
 };
 
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
 // MAXNT = launch bound (threads), SMAX = staging quads per thread per round.
-// NTC = the thread count as a compile-time constant (0: blockDim.x at run time).
+// NTC = the thread count as a compile-time constant (0: blockDim.x at run time);
+// NTC = kResTailNT (512): the eight-wave build (affinities in VGPRs, tail pixels).
 // GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
 // folds away, and with it the setup spill slots it costs).
 template <typename T, int MAXNT, int SMAX, int NTC, bool GROUPS>
@@ -302,7 +352,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // With a compile-time thread count the window size is one too (res_win_cells),
     // so every fwinB access is an immediate offset from its fwin address.
     const int NT = NTC ? NTC : (int)blockDim.x;
-    const int WC = NTC ? res_win_cells(NTC) : a.win_cells;
+    const int WC = NTC == kResTailNT ? kResTailWC : NTC ? res_win_cells(NTC) : a.win_cells;
     // PITCH: the window's row pitch as a compile-time constant (576-thread builds: the
     // second footprint row is a ds_read immediate offset, and the window cells are kept as
     // 16-bit byte addresses, so a tap spends one VALU on its address instead of three)
@@ -315,6 +365,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // (1 with conf_prop off) and dep (0 with preserve off) — every one an immediate
     // offset from ONE address register.
     float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
+    // the eight-wave build: the quad's affinities and 1 - sum in VGPRs (aq), its conf' / dep
+    // in two float4 planes of NT (cdl), the tail pixels' values in K + 3 planes of 256 (tal)
+    constexpr bool TAIL = NTC == kResTailNT;
+    constexpr int SM = TAIL ? kResTailSMax : SMAX;  // staging quads per thread per round
+    float4 *cdl = reinterpret_cast<float4 *>(fwinB + WC);
+    float *tal = reinterpret_cast<float *>(cdl + 2 * NT) + (tid - 256);
 
     gu32 *sync = (gu32 *)(a.sync);
     const int ngroups = GROUPS && a.ngroups > 1 ? a.ngroups : 1;
@@ -367,7 +423,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         res_wtrace(a.pred, a.T, __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u), 0)[0] = hw;
     }
-    const bool active = tid < nown;
+    // TAIL: the threads own the part's first NT quads as quads, the rest as tail pixels (below)
+    const int nq_main = TAIL ? min(nown, NT) : nown;
+    const bool active = tid < nq_main;
     // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned): every
     // part publishes the XCC it runs on; if all parts of its image share one, the image's
     // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed: the word
@@ -395,7 +453,25 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         x0 = 4 * (c0 + tid - rr * nqw);
     }
     const unsigned vpix = (unsigned)(y * W + x0) * ES;
+    // ---- TAIL: pixel tj of the quads beyond the first NT (row-major in the part), one per
+    // lane of waves 4..7 — one wave of each SIMD — in four contiguous chunks (consecutive
+    // lanes hold consecutive pixels, so the wave's dword stores coalesce)
+    const int ntail = TAIL ? 4 * (nown - nq_main) : 0;
+    const int tchunk = (ntail + 3) >> 2;
+    const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave (uniform)
+    const int tj = (wvu - 4) * tchunk + lane;
+    const bool tail_on = TAIL && wvu >= 4 && lane < tchunk && tj < ntail;
+    const bool tail_wave = TAIL && wvu >= 4 && (wvu - 4) * tchunk < ntail;  // wave-uniform
+    int ty = r0, tx = 4 * c0;
+    if (tail_on) {
+        const int q = NT + (tj >> 2), rr = q / nqw;
+        ty = r0 + rr;
+        tx = 4 * (c0 + q - rr * nqw) + (tj & 3);
+    }
+    const unsigned tvpix = (unsigned)(ty * W + tx) * ES;
     float hy[K][4], hx[K][4];
+    float4 aq[K + 1];          // TAIL: the quad's affinities and 1 - sum (what akl holds otherwise)
+    float thy[K] = {}, thx[K] = {};  // TAIL: the tail pixel's sample coordinates
     {
         float dv[4];
         float ak[K][4], aref[4];
@@ -422,12 +498,44 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
+        // (the eight-wave build: in VGPRs, two waves per SIMD leave 256 per lane)
+        if constexpr (TAIL) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
-        akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-        akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
-        akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+            for (int k = 0; k < K; ++k) aq[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
+            aq[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+            cdl[tid] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+            cdl[NT + tid] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
+            akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+            akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+            akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+        }
+        if (TAIL && wvu >= 4) {  // the tail pixel's invariants (lanes without one load pixel (r0, 4 c0): unused)
+            float taf[K + 3];
+            float s = 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                taf[k] = ResVec<T>::template load1<0>(ra_, tvpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes);
+                const int ok = (off_ins && k >= REF) ? k + 1 : k;
+                thy[k] = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)(2 * ok) * plane_bytes);
+                thx[k] = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)(2 * ok + 1) * plane_bytes);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) s += taf[k];
+            taf[K] = 1.0f - s;
+            taf[K + 1] = has_conf ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), tvpix, 0u) : 1.f;
+            taf[K + 2] = preserve ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), tvpix, 0u) : 0.f;
+#pragma unroll
+            for (int k = 0; k < K + 3; ++k) tal[256 * k] = taf[k];
+        }
     }
+    // the quad's row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
+    const auto aff4 = [&](const int k) -> float4 {
+        if constexpr (TAIL) return k <= K ? aq[k < K + 1 ? k : 0] : cdl[(k - K - 1) * NT + tid];
+        else return akl[k];
+    };
 
     // ---- the window: the rectangle of every cell a valid tap of this part touches
     // (offsets are invariant, so once), when it fits the LDS cells allocated;
@@ -461,6 +569,22 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
         }
+        if (TAIL) {  // the tail pixel's taps
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
+                const float h_im = (float)(ty - PH + i) + thy[k];
+                const float w_im = (float)(tx - PW + jj) + thx[k];
+                thy[k] = h_im;
+                thx[k] = w_im;
+                if (tail_on && h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                    hmn = fminf(hmn, h_im);
+                    hmx = fmaxf(hmx, h_im);
+                    wmn = fminf(wmn, w_im);
+                    wmx = fmaxf(wmx, w_im);
+                }
+            }
+        }
         int mn = r0, mx = r1, cmn = 4 * c0, cmx = 4 * c1;
         if (hmn <= hmx) {
             mn = min(mn, (int)floorf(hmn));
@@ -468,7 +592,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             cmn = min(cmn, (int)floorf(wmn));
             cmx = max(cmx, (int)floorf(wmx) + 1);
         }
-        res_span_merge(ctl, active, mn, mx, cmn, cmx);
+        res_span_merge(ctl, active || tail_on, mn, mx, cmn, cmx);
     }
     lds_barrier();
     int rlo = ctl[1], rhi = ctl[2], wq0 = ctl[3] >> 2, wq1 = ctl[4] >> 2;  // >> 2: floor for negatives too
@@ -534,8 +658,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
     }
+    bool has_fb_t = false;  // TAIL: the tail pixel has a tap outside the window
+    if (TAIL) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float h_im = thy[k], w_im = thx[k];
+            if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                if (!((unsigned)(h_low - rlo) < (unsigned)(WH - 1) && (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)))
+                    has_fb_t = true;
+            } else {
+                thy[k] = (float)rlo;
+                thx[k] = (float)(4 * wq0 - PADX);
+            }
+        }
+        has_fb_t = has_fb_t && tail_on && !dynwin;
+    }
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
-    const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
+    const bool wave_fb = __ballot(has_fb || has_fb_t) != 0;  // wave-uniform: this wave has general-path lanes
     // Every tap's bilinear geometry is iteration-invariant, so it is resolved once:
     // the fractional parts lh = h - floor(h), lw = w - floor(w) (.cuh:35-36, the same
     // values the per-iteration form computes) and the window cell of the footprint's
@@ -567,6 +707,27 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
     }
 
+    float tlh[K], tlw[K];  // TAIL: the tail pixel's tap geometry (the same resolution)
+    unsigned tadp[K / 2];
+    int town = 0;          // TAIL: window cell of the tail pixel
+    if (TAIL) {
+        const float WWf = (float)WW;
+        const int lbase = PADX - 4 * wq0 - rlo * WW, bofs = WC - 1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float fh = floorf(thy[k]), fw = floorf(thx[k]);
+            tlh[k] = thy[k] - fh;
+            tlw[k] = thx[k] - fw;
+            int li = (int)(fh * WWf + fw) + lbase;
+            li = ((unsigned)li < (unsigned)(WH * WW)) ? li : 0;
+            unsigned idx = (li & 1) ? (unsigned)(li + bofs) : (unsigned)li;
+            idx = 4u * ((unsigned)kResCtl + idx);  // (a PITCH build: LDS byte addresses)
+            if (k & 1) tadp[k >> 1] |= idx << 16;
+            else tadp[k >> 1] = idx;
+        }
+        town = (ty - rlo) * WW + tx - 4 * wq0 + PADX;
+    }
+
     // Staging map (iterations t >= 2): the in-image window quads outside the own
     // rectangle — the bands above and below it (full window width), then the
     // columns left and right of it.  Iteration 1 stages the whole in-image window.
@@ -596,7 +757,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // plane t.  Plane 0 is step 1's output (the launch's input: never poisoned), so the
     // first iteration stages without waiting.  The XCC ids are read by the last wave holding
     // quads (any wave would do).
-    const int pwave = (nown - 1) >> 6;
+    const int pwave = (nq_main - 1) >> 6;
     bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in the first iteration)
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     int t_abort = 0;
@@ -605,6 +766,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                                        ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
         const rsrc_t rp = make_rsrc(p_all + (size_t)(t - 1) * a.tstride + b * HW);
+        // ---- the inserted-offset copy (ResArgs::off_out): output plane t - 1 (a raw plane, or
+        // the reference tap's zero plane) loaded here, stored after the staging phase (by then
+        // the staging waits have covered the load)
+        const int cpc = t - 1;
+        const bool cpy = a.off_out != nullptr && cpc < 2 * (K + 1);
+        const int cptt = cpc >> 1;
+        const int cpsrc = cptt == REF ? -1 : 2 * (cptt < REF ? cptt : cptt - 1) + (cpc & 1);
+        float cpq[4] = {0.f, 0.f, 0.f, 0.f}, cpq1 = 0.f;
+        if (cpy && cpsrc >= 0) {
+            const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+            if (active) ResVec<T>::template load<0>(ro, vpix, (unsigned)cpsrc * plane_bytes, cpq);
+            if (tail_on) cpq1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)cpsrc * plane_bytes);
+        }
         // ---- a launch's first iteration: the hand-off mode of this image (all its parts
         // on this part's XCC: L2), decided from the published XCC ids, identically by
         // every part of the image; its stores use it
@@ -642,13 +816,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int nsq_it = (exp_dbg(a.dbg) & 2u) ? 0 : (rim ? nrest : nall);
         bool nonfin = false;  // this thread staged a non-finite f
-        for (int base = tb; base < nsq_it; base += SMAX * NT) {
-            float sv[SMAX][4], cv[SMAX][4];
-            int sl[SMAX];
-            unsigned gq[SMAX];
+        for (int base = tb; base < nsq_it; base += SM * NT) {
+            float sv[SM][4], cv[SM][4];
+            int sl[SM];
+            unsigned gq[SM];
             bool ok = true;  // every staged quad of this lane holds this call's values
 #pragma unroll
-            for (int s = 0; s < SMAX; ++s) {
+            for (int s = 0; s < SM; ++s) {
                 const int k = base + s * NT;
                 int r, c;  // window quad: row, quad column
                 if (!rim) {
@@ -673,7 +847,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     if (!ok) {
                         ok = true;
 #pragma unroll
-                        for (int s = 0; s < SMAX; ++s)
+                        for (int s = 0; s < SM; ++s)
                             if (base + s * NT < nsq_it) ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
                     }
                     if (++spins > kResSpinLimit ||
@@ -687,7 +861,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
 #pragma unroll
-            for (int s = 0; s < SMAX; ++s) {
+            for (int s = 0; s < SM; ++s) {
                 const int k = base + s * NT;
                 if (k < nsq_it) {
                     float4 f = make_float4(sv[s][0], sv[s][1], sv[s][2], sv[s][3]);
@@ -713,6 +887,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             t_abort = t;
             break;
         }
+        if (cpy) {  // streaming (nt): an output only
+            const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
+            if (active) ResVec<T>::template store<kNT>(rco, vpix, (unsigned)cpc * plane_bytes, cpq);
+            if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)cpc * plane_bytes, cpq1);
+            if (t == a.T - 1) {  // a short section: the planes past T - 1, here
+                const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+                for (int c = t; c < 2 * (K + 1); ++c) {
+                    const int tt = c >> 1, src = tt == REF ? -1 : 2 * (tt < REF ? tt : tt - 1) + (c & 1);
+                    float q[4] = {0.f, 0.f, 0.f, 0.f}, q1 = 0.f;
+                    if (src >= 0) {
+                        if (active) ResVec<T>::template load<0>(ro, vpix, (unsigned)src * plane_bytes, q);
+                        if (tail_on) q1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)src * plane_bytes);
+                    }
+                    if (active) ResVec<T>::template store<kNT>(rco, vpix, (unsigned)c * plane_bytes, q);
+                    if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)c * plane_bytes, q1);
+                }
+            }
+        }
         // the window holds a non-finite f (staged now, or an own quad written back after
         // the previous iteration): the reference tap takes the four-corner form below
         const bool refull = __builtin_amdgcn_readfirstlane(ctl[6 + (t & 1)]) != 0;
@@ -722,6 +914,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (active && t + 2 < a.T) {
             if (l2) ResVec<T>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
             else ResVec<T>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
+        }
+        if (tail_on && t + 2 < a.T) {
+            if (l2) ResVec<T>::template poison1<0>(make_rsrc(p_out + a.tstride), tvpix);
+            else ResVec<T>::template poison1<kSc1>(make_rsrc(p_out + a.tstride), tvpix);
         }
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
@@ -733,8 +929,113 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
             asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
+            if (TAIL) asm volatile("" : "+v"(tlh[k]), "+v"(tlw[k]));
         }
+        if (TAIL)
+#pragma unroll
+            for (int k = 0; k < K / 2; ++k) asm volatile("" : "+v"(tadp[k]));
         float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
+        // The general path's tap sum of one pixel (y, x) (window cell lcell, byte offset gvo):
+        // every tap in tap order with the reference tap (weight 1 - sum, the setup's order) at
+        // K/2, in the reference's per-corner form where its footprint leaves the window.
+        // A corner spin that times out (or sees another part's abort: polled every 16
+        // spins) raises the abort like the staging spin's, and the lane stops spinning on
+        // later corners (gp_fail); the poison then reaches the sum as a NaN, and the abort
+        // fill below the loop covers the later planes.
+        bool gp_fail = false;
+        // Affinity k and 1 - sum from LDS (arow[k * astep], arow[K * astep]), or, with arow null
+        // (the eight-wave build's quads: their rows are in VGPRs), re-read from global memory.
+        const auto gp_pixel = [&](const int gy, const int gx, const int lcell, const unsigned gvo, const float *arow,
+                                  const int astep) -> float {
+            const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+            const rsrc_t rg = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
+            const bool glb = TAIL && arow == nullptr;
+            float s = 0.f;
+#pragma unroll 1
+            for (int k = 0; k < K; ++k) {
+                if (k == REF) {
+                    float ar;
+                    if (glb) {
+                        float sa = 0.f;
+#pragma unroll 1
+                        for (int k2 = 0; k2 < K; ++k2)
+                            sa += ResVec<T>::template load1<0>(rg, gvo, (unsigned)(k2 < REF ? k2 : k2 + 1) * plane_bytes);
+                        ar = 1.0f - sa;
+                    } else {
+                        ar = arow[K * astep];
+                    }
+                    s += fwin[lcell] * ar;
+                }
+                const float av = glb ? ResVec<T>::template load1<0>(rg, gvo, (unsigned)(k < REF ? k : k + 1) * plane_bytes)
+                                     : arow[k * astep];
+                const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
+                const int ok = (off_ins && k >= REF) ? k + 1 : k;
+                const float h_im = (float)(gy - PH + i) + ResVec<T>::template load1<0>(ro, gvo, (unsigned)(2 * ok) * plane_bytes);
+                const float w_im = (float)(gx - PW + jj) + ResVec<T>::template load1<0>(ro, gvo, (unsigned)(2 * ok + 1) * plane_bytes);
+                float v = 0.f;
+                if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                    const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                    const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                    const float hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    if ((unsigned)(h_low - rlo) < (unsigned)(WH - 1) && (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)) {
+                        const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
+                        v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
+                    } else {
+                        const int h_high = h_low + 1, w_high = w_low + 1;
+                        float c4[4];
+                        const int cy[4] = {h_low, h_low, h_high, h_high};
+                        const int cx[4] = {w_low, w_high, w_low, w_high};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            c4[u] = 0.f;
+                            if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
+                                const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
+                                float pv = 0.f;
+                                for (unsigned sp = 0;; ++sp) {  // per lane, bounded
+                                    bool rdy;
+                                    pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
+                                    if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
+                                    if (sp > kResSpinLimit ||
+                                        ((sp & 15u) == 15u &&
+                                         __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+                                        gp_fail = true;
+                                        break;
+                                    }
+                                    __builtin_amdgcn_s_sleep(1);
+                                }
+                                c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                            }
+                        }
+                        v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
+                    }
+                }
+                s += v * av;
+            }
+            return s;
+        };
+        const auto gp_raise = [&]() {  // a general-path spin timed out: the abort (rare lanes)
+            if (gp_fail) {
+                ctl[0] = 1;
+                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        };
+        // TAIL: the tail pixel's taps (tail waves: lanes with a tail pixel), after the quad's
+        // (its reads interleaved into the quad's slot loop spilled: 256 VGPRs + 64 in scratch)
+        float tacc = 0.f;
+        const auto tail_tap = [&](const int k) {
+            if (k == REF) tacc += fwin[town] * tal[256 * K];
+            const unsigned idx = (k & 1) ? (tadp[k >> 1] >> 16) : (tadp[k >> 1] & 0xffffu);
+            const float2 s01 = lds_pair(idx);
+            __builtin_amdgcn_sched_barrier(0);
+            const float2 s23 = lds_pair(idx + 4u * PITCH);
+            const float lh = tlh[k], lw = tlw[k];
+            const float hh = 1.f - lh, hw = 1.f - lw;
+            const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+            const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
+            tacc += v * tal[256 * k];
+        };
         if (active && !(exp_dbg(a.dbg) & 4u)) {
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             // branch-free path: every tap from the LDS window (invalid taps read zeros), in
@@ -755,9 +1056,9 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                           // form is applied after the taps, below)
             auto issue = [&](const int s) {
                 const int k = s >> 2, e = s & 3;
-                if (e == 0) akv[k] = akl[k];
+                if (e == 0) akv[k] = aff4(k);
                 if (s == 4 * REF) {  // the reference tap's own-quad cells and weight
-                    akv[K] = akl[K];
+                    akv[K] = aff4(K);
                     cref = *reinterpret_cast<const float4 *>(&fwin[lown]);
                 }
                 const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
@@ -819,84 +1120,80 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // general path (rare; only waves holding a tap outside the window): the
             // reference's per-corner checks, from global memory where needed (the same
             // cells every iteration, re-loaded until not the poison, as the staging's).  It
-            // re-reads its offsets from global memory and runs a rolled tap loop, so it
-            // shares no registers with the branch-free path (no spills around it).
-            // A corner spin that times out (or sees another part's abort: polled every 16
-            // spins) raises the abort like the staging spin's, and the lane stops spinning on
-            // later corners (gp_fail); the poison then reaches the sum as a NaN, and the abort
-            // fill below the loop covers the later planes.
-            bool gp_fail = false;
+            // re-reads its offsets and affinities from global memory and runs a rolled tap
+            // loop, so it shares no registers with the branch-free path (no spills around it).
             if (kResGeneralPath && wave_fb && has_fb && !(exp_dbg(a.dbg) & 64u)) {
-                const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
                 // the own quad's row and first column, recomputed from its byte offset (not
                 // live across the loop)
                 const int pe = (int)(vpix / ES), y = pe / W, x0 = pe - y * W;
+                if constexpr (TAIL) {  // (the quad's affinities are in VGPRs: re-read from global memory)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float s = 0.f;
-#pragma unroll 1
-                    for (int k = 0; k < K; ++k) {
-                        if (k == REF) {
-                            const float4 ar = akl[K];
-                            const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
-                            s += fwin[lown + e] * arv[e];
-                        }
-                        const float4 a4 = akl[k];
-                        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-                        const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
-                        const int ok = (off_ins && k >= REF) ? k + 1 : k;
-                        const float h_im = (float)(y - PH + i) +
-                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok) * plane_bytes);
-                        const float w_im = (float)(x0 + e - PW + jj) +
-                                           ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok + 1) * plane_bytes);
-                        float v = 0.f;
-                        if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                            const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
-                            const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
-                            const float hh = 1.f - lh, hw = 1.f - lw;
-                            const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                            if ((unsigned)(h_low - rlo) < (unsigned)(WH - 1) &&
-                                (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)) {
-                                const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
-                                v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
-                            } else {
-                                const int h_high = h_low + 1, w_high = w_low + 1;
-                                float c4[4];
-                                const int cy[4] = {h_low, h_low, h_high, h_high};
-                                const int cx[4] = {w_low, w_high, w_low, w_high};
-#pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    c4[u] = 0.f;
-                                    if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
-                                        const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                        float pv = 0.f;
-                                        for (unsigned sp = 0;; ++sp) {  // per lane, bounded
-                                            bool rdy;
-                                            pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
-                                            if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
-                                            if (sp > kResSpinLimit ||
-                                                ((sp & 15u) == 15u &&
-                                                 __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-                                                gp_fail = true;
-                                                break;
-                                            }
-                                            __builtin_amdgcn_s_sleep(1);
-                                        }
-                                        c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
-                                    }
-                                }
-                                v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
+                    for (int e = 0; e < 4; ++e) acc[e] = gp_pixel(y, x0 + e, lown + e, vpix + e * ES, nullptr, 0);
+                } else {  // (the same sum written out: as the lambda, the 128-thread build spilled)
+                    const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float s = 0.f;
+    #pragma unroll 1
+                        for (int k = 0; k < K; ++k) {
+                            if (k == REF) {
+                                const float4 ar = akl[K];
+                                const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
+                                s += fwin[lown + e] * arv[e];
                             }
+                            const float4 a4 = akl[k];
+                            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                            const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
+                            const int ok = (off_ins && k >= REF) ? k + 1 : k;
+                            const float h_im = (float)(y - PH + i) +
+                                               ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok) * plane_bytes);
+                            const float w_im = (float)(x0 + e - PW + jj) +
+                                               ResVec<T>::template load1<0>(ro, vpix + e * ES, (unsigned)(2 * ok + 1) * plane_bytes);
+                            float v = 0.f;
+                            if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
+                                const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
+                                const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
+                                const float hh = 1.f - lh, hw = 1.f - lw;
+                                const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                                if ((unsigned)(h_low - rlo) < (unsigned)(WH - 1) &&
+                                    (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)) {
+                                    const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
+                                    v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
+                                } else {
+                                    const int h_high = h_low + 1, w_high = w_low + 1;
+                                    float c4[4];
+                                    const int cy[4] = {h_low, h_low, h_high, h_high};
+                                    const int cx[4] = {w_low, w_high, w_low, w_high};
+    #pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        c4[u] = 0.f;
+                                        if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
+                                            const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
+                                            float pv = 0.f;
+                                            for (unsigned sp = 0;; ++sp) {  // per lane, bounded
+                                                bool rdy;
+                                                pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
+                                                if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
+                                                if (sp > kResSpinLimit ||
+                                                    ((sp & 15u) == 15u &&
+                                                     __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+                                                    gp_fail = true;
+                                                    break;
+                                                }
+                                                __builtin_amdgcn_s_sleep(1);
+                                            }
+                                            c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                                        }
+                                    }
+                                    v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
+                                }
+                            }
+                            s += v * av[e];
                         }
-                        s += v * av[e];
+                        acc[e] = s;
                     }
-                    acc[e] = s;
                 }
-            }
-            if (gp_fail) {  // (rare lanes; every writer stores 1)
-                ctl[0] = 1;
-                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                gp_raise();
             }
             // the reference tap in the reference's four-corner form (.cuh:37-52: the integer
             // point's weights are exactly (1, 0, 0, 0)) differs from the one-cell form used
@@ -913,7 +1210,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                         acc[e] = __builtin_nanf("");
             }
             float o[4], fin[4];
-            const float4 d4 = akl[K + 2];
+            const float4 d4 = aff4(K + 2);
             const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -934,6 +1231,40 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
                 ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
+                }
+        // ---- TAIL: the tail pixel (waves 4..7, one per SIMD), the same arithmetic in the
+        // same order: taps 0..K-1 with the reference tap (one-cell form) at K/2
+        float pown_t = 0.f;
+        if (tail_wave && !(exp_dbg(a.dbg) & 4u)) {
+            if (tail_on) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) tail_tap(k);
+                float acc = tacc;
+                if (kResGeneralPath && has_fb_t && !(exp_dbg(a.dbg) & 64u)) {
+                    const int pe = (int)(tvpix / ES), gy = pe / W, gx = pe - gy * W;
+                    acc = gp_pixel(gy, gx, town, tvpix, tal, 256);
+                    gp_raise();
+                }
+                if (refull) {  // the four-corner reference tap (see the quad's form above)
+                    const float *r0p = &fwin[town], *r1p = r0p + WW;
+                    if (!__builtin_isfinite(r0p[1]) || !__builtin_isfinite(r1p[0]) || !__builtin_isfinite(r1p[1]))
+                        acc = __builtin_nanf("");
+                }
+                float vv = acc;
+                if (preserve) {
+                    const float dt = tal[256 * (K + 2)];
+                    const float m = dt > 0.f ? 1.f : 0.f;
+                    vv = (1.0f - m) * vv + m * dt;
+                }
+                if (clip) vv = clamp0(vv);
+                const float fin = clip ? vv : clamp0(vv);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its plane-(t+1) poison acknowledged
+                if (l2) ResVec<T>::template store1<0>(make_rsrc(p_out), tvpix, 0u, vv);
+                else ResVec<T>::template store1<kSc1>(make_rsrc(p_out), tvpix, 0u, vv);
+                pown_t = round_to<T>(vv);
+                if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
+                    ResVec<T>::template store1<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), tvpix, 0u, fin);
+            }
         }
         if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
         if (kResWTrace && trace && lane == 0) res_wtrace(a.pred, a.T, wbase, t)[0] = __builtin_amdgcn_s_memrealtime();
@@ -944,7 +1275,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- the own quad's f_t = p_t * conf' straight into the window, as the next
         // staging would load it
         if (t < a.T - 1 && active && !(exp_dbg(a.dbg) & 2u)) {
-            const float4 cw = akl[K + 1];
+            const float4 cw = aff4(K + 1);
             float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
             if (has_conf) {
                 f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
@@ -955,6 +1286,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             fwinB[lown + 2] = f.w;
             if (!__builtin_isfinite((f.x + f.y) + (f.z + f.w)))
                 ctl[6 + ((t + 1) & 1)] = 1;  // (benign race: every writer stores 1)
+        }
+        if (tail_on && t < a.T - 1 && !(exp_dbg(a.dbg) & 2u)) {  // TAIL: the tail pixel's f_t
+            const float f = has_conf ? pown_t * tal[256 * (K + 1)] : pown_t;
+            fwin[town] = f;
+            fwinB[town - 1] = f;
+            if (!__builtin_isfinite(f)) ctl[6 + ((t + 1) & 1)] = 1;
         }
     }
     // aborted: NaN in every plane this part has not written (this group's remaining
@@ -969,6 +1306,15 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 for (int tt = g2 == grp ? t_abort : 1; tt < a.T; ++tt)
                     ResVec<T>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
                 ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
+            }
+        }
+        if (tail_on) {
+            for (int g2 = grp; g2 < ngroups; ++g2) {
+                const int b2 = bl + g2 * a.B;
+                for (int tt = g2 == grp ? t_abort : 1; tt < a.T; ++tt)
+                    ResVec<T>::template store1<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), tvpix, 0u,
+                                                     __builtin_nanf(""));
+                ResVec<T>::template store1<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), tvpix, 0u, __builtin_nanf(""));
             }
         }
         return;

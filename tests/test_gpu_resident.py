@@ -65,12 +65,16 @@ def _nan_equal(x, y):
 def _both(inp, T=18, nan_ok=False, **kw):
     """(resident, steps): the default resident form (behind a step-1 launch), checked
     here against the resident form with every hand-off write-through (NLSPN_RES_L2=0: no
-    image's hand-offs kept in an XCD's L2), and the step form.
+    image's hand-offs kept in an XCD's L2) and against the nine-wave build where the
+    eight-wave one applies (NLSPN_RES_TAIL), and the step form.
     nan_ok: NaN results compare by position (_nan_equal)."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
         with _env("0", "NLSPN_RES_L2"):
             c = propagate(*inp, prop_time=T, **kw)
+        # the other of the eight- and nine-wave builds where the eight-wave one applies
+        with _env("0" if _lib_tail_default() else "1", "NLSPN_RES_TAIL"):
+            d = propagate(*inp, prop_time=T, **kw)
     with _env("0"):
         b = propagate(*inp, prop_time=T, **kw)
     torch.cuda.synchronize()
@@ -81,7 +85,19 @@ def _both(inp, T=18, nan_ok=False, **kw):
     eq = _nan_equal if nan_ok else _bits_equal
     assert eq(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
     assert eq(a["pred"], c["pred"])
+    assert eq(a["pred_inter_tensor"], d["pred_inter_tensor"]), "eight-wave and nine-wave builds differ"
+    assert eq(a["pred"], d["pred"])
     return a, b
+
+
+def _lib_tail_default():
+    """Whether the library plans the eight-wave build by default at the C2 shape."""
+    old = os.environ.pop("NLSPN_RES_TAIL", None)
+    try:
+        return resident_config(8, 228, 304)[2] == 512
+    finally:
+        if old is not None:
+            os.environ["NLSPN_RES_TAIL"] = old
 
 
 def _bits_equal(x, y):
@@ -93,9 +109,17 @@ def _bits_equal(x, y):
 def test_resident_engaged_at_c2():
     with _env("1"):
         ok, grid, block, lds = resident_config(8, 228, 304)
-        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
+        assert ok and grid == 256 and block in (512, 576) and lds > 80 * 1024
         ok, grid, block, lds = resident_config(4, 240, 1216)  # C3: two launches of 2 images x 128 parts
-        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
+        assert ok and grid == 256 and block in (512, 576) and lds > 80 * 1024
+        # C2 / C3 shapes: the nine-wave build, or the eight-wave one (512 threads, quads + tail
+        # pixels; fp32)
+        with _env("1", "NLSPN_RES_TAIL"):
+            assert resident_config(8, 228, 304)[2] == 512
+            assert resident_config(4, 240, 1216)[2] == 512
+            assert resident_config(8, 228, 304, dtype=1)[2] == 576  # fp16: the nine-wave build
+        with _env("0", "NLSPN_RES_TAIL"):
+            assert resident_config(8, 228, 304)[2] == 576
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
         ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in 13 x 19 parts of 72 quads
         assert ok and grid == 247 and block == 128
@@ -106,6 +130,7 @@ def test_resident_engaged_at_c2():
     (8, 228, 304, 2.0, torch.float32, True, {"always_clip": True}),
     (8, 228, 304, 2.0, torch.float32, False, {"preserve_input": False}),
     (8, 228, 304, 2.0, torch.float16, True, {}),                        # fp16 storage
+    (8, 228, 304, 12.0, torch.float32, True, {"always_clip": True}),    # C2 parts, fixed halo: tail pixels' general path
     (4, 96, 128, 12.0, torch.float32, True, {}),                        # taps beyond the halo
     (2, 64, 96, 60.0, torch.float32, True, {"affinity": "TC"}),         # mostly out of image, long ranges
     (1, 24, 32, 2.0, torch.float32, True, {}),                          # 3 tiny parts
@@ -220,7 +245,7 @@ def test_resident_replays_stable_and_no_abort():
     (8, 228, 304, "1", torch.float32, 3.0), (8, 228, 304, "0", torch.float32, 3.0),
     (4, 240, 1216, "1", torch.float32, 3.0), (1, 228, 304, "1", torch.float32, 3.0),
     (8, 228, 304, "1", torch.float16, 3.0),
-    (4, 96, 128, "1", torch.float32, 12.0), (2, 120, 2048, "1", torch.float32, 12.0)])
+    (8, 228, 304, "1", torch.float32, 12.0), (2, 120, 2048, "1", torch.float32, 12.0)])
 def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype, sigma):
     """Replays over in-place refilled inputs that alternate between two data sets: every
     plane a hand-off reads was last written with the OTHER set's values, so a consumer that
@@ -390,7 +415,7 @@ def test_product_library_ignores_experiment_switches():
     assert torch.equal(o, ref)
 
 
-@pytest.mark.parametrize("B,H,W,sigma", [(4, 96, 128, 12.0), (2, 120, 2048, 12.0)])
+@pytest.mark.parametrize("B,H,W,sigma", [(8, 228, 304, 12.0), (2, 120, 2048, 12.0)])
 def test_general_path_taken_at_fixed_halo_shapes(B, H, W, sigma):
     """The fixed-halo shapes of the alternating-input test do take the general path (its
     results change when the experiments build switches that path off)."""

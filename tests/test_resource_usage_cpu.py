@@ -67,7 +67,11 @@ def test_resident_kernel_registers_and_scratch():
     assembly)."""
     rows = _rows()
     res = {n: r for n, r in rows.items() if "prop_resident_kernel" in n}
-    assert res and all(r["VGPRs"] <= 168 and r.get("Occupancy", 0) >= 3 for r in res.values()), res
+    # the eight-wave build (launch bound 512: two waves per SIMD, 256 VGPRs per lane)
+    eight = lambda n: "Li512ELi1ELi512E" in n  # noqa: E731
+    assert res and all((r["VGPRs"] <= 256 and r.get("Occupancy", 0) >= 2) if eight(n) else
+                       (r["VGPRs"] <= 168 and r.get("Occupancy", 0) >= 3) for n, r in res.items()), res
+    assert any(eight(n) for n in res), "eight-wave builds missing"
     assert any("ELi576E" in n for n in res) and any("ELi128E" in n for n in res), "fixed thread-count builds missing"
     assert any(_groups(n) for n in res) and any(not _groups(n) for n in res), "GROUPS builds missing"
     assert all(r.get("ScratchSize", 0) <= (RESIDENT_SCRATCH_CAP_GROUPS if _groups(n) else RESIDENT_SCRATCH_CAP)
