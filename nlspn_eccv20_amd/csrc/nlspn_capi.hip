@@ -24,16 +24,18 @@
 
 // defined in nlspn_kern_resident.hip (own translation unit and flags)
 namespace nlspn {
-#define NLSPN_RES_EXTERN(T)                                                       \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>(ResArgs);    \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
-NLSPN_RES_EXTERN(float)
-NLSPN_RES_EXTERN(__half)
-extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>(ResArgs);
-extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>(ResArgs);
+#define NLSPN_RES_EXTERN(T, F)                                                       \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>(ResArgs);    \
+    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
+NLSPN_RES_EXTERN(float, true)
+NLSPN_RES_EXTERN(__half, true)
+NLSPN_RES_EXTERN(float, false)
+NLSPN_RES_EXTERN(__half, false)
+extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
 #define NLSPN_HD_EXTERN(MB)                                            \
     extern template __global__ void heads_kernel<MB, true>(HeadsArgs); \
@@ -325,7 +327,18 @@ int res_guard_after(hipStream_t s) {
 
 constexpr int kResMaxGroups = 64;  // image groups (back-to-back resident launches) per section
 
+// The prologue's inputs and outputs, for a resident plan that runs it inside the launch
+// (kResFirst): then no step-1 launch precedes the resident launches.
+struct ResFirst {
+    const void *pinit, *conf_raw, *aff_raw;
+    long long aff_bs;
+    const float *gamma;
+    int kind;
+    void *aff_out, *conf_out;  // conf_out null iff conf_raw null
+};
+
 struct ResPlan {
+    bool first = false;  // the prologue and iteration 1 run inside the launches
     const void *fn = nullptr;
     const void *fn_merged = nullptr;  // launch 0's kernel when it runs several image groups
     unsigned block = 0;
@@ -336,21 +349,27 @@ struct ResPlan {
     ResArgs a[kResMaxGroups];
 };
 
+template <typename T, bool F>
+const void *res_fn_f(long long nt, bool groups) {
+    if (groups)
+        return nt == 576 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>)
+                         : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>);
+    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>);
+    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>);
+    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>);
+}
+
+// first: the build with the forward prologue and iteration 1 inside the launch (kResFirst)
 template <typename T>
-const void *res_fn(long long nt, bool groups, bool pitch_ok, bool tail) {
+const void *res_fn(long long nt, bool groups, bool pitch_ok, bool tail, bool first) {
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
-    if (tail) {  // the eight-wave build (fp32 only; the planner checked its pitch)
-        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>);
-        return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>);
+    if (tail) {  // the eight-wave build (fp32 only; the planner checked its pitch; no prologue form)
+        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>);
+        return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>);
     }
-    if (groups)
-        return nt == 576 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>)
-                         : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>);
-    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>);
-    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>);
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>);
+    return first ? res_fn_f<T, true>(nt, groups) : res_fn_f<T, false>(nt, groups);
 }
 
 // The part grid of a resident launch: Bg images per launch, each cut into gy row
@@ -404,7 +423,7 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
 // Fills P and returns true when the resident kernel applies (iterations 2..T).
 bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void *aff_norm, const void *off_raw,
                    long long off_bs, void *pred_inter, void *pred, void *workspace, int B, int H, int W, int kh,
-                   int kw, int T, unsigned flags, ResPlan &P, void *off_out = nullptr) {
+                   int kw, int T, unsigned flags, ResPlan &P, void *off_out = nullptr, const ResFirst *fp = nullptr) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
@@ -412,6 +431,12 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
         return false;
+    // the prologue in the launch: raw inputs and prologue outputs 16-B aligned, raw offset layout
+    if (fp && (!aligned(fp->pinit, vb) || !aligned(fp->conf_raw, vb) || !aligned(fp->aff_raw, vb) ||
+               !aligned(fp->aff_out, vb) || !aligned(fp->conf_out, vb) || !aligned(off_out, vb) ||
+               fp->aff_bs % 4 != 0 || !fp->gamma ||
+               !fp->aff_out || (flags & kResOffInserted)))
+        fp = nullptr;
     const int cus = device_cus();
     if (cus < 1) return false;
     const long long HW = (long long)H * W;
@@ -450,14 +475,17 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (tail) {
         S.nt = kResTailNT;
         S.win_cells = kResTailWC;
+        fp = nullptr;  // (the eight-wave build has no prologue form: step 1 runs before it)
     }
+    P.first = fp != nullptr;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded); the eight-wave build keeps
     // conf' / dep planes and the tail pixels' planes instead of per-thread rows
     const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : 16 * kResAS * (size_t)S.nt),
                                         80 * 1024 + 16);
     if (lds > (size_t)kResLds) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false, pitch_ok, tail) : res_fn<__half>(S.nt, false, pitch_ok, false);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false, pitch_ok, tail, P.first)
+                                    : res_fn<__half>(S.nt, false, pitch_ok, false, P.first);
     P.block = (unsigned)S.nt;
     P.lds = lds;
     P.sync_bytes = (size_t)(G + 1) * 4 * kResLine;
@@ -493,7 +521,18 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                          flags | (l2ok ? kResL2 : 0u), dbg};
         // the output dict's inserted offsets copied by the resident loop (ResArgs::off_out)
         // instead of step 1; NLSPN_RES_OFFCOPY=0 (A/B) leaves them to step 1
-        if (copy_off) P.a[k].off_out = const_cast<void *>(at(off_out, b0 * 2 * (K + 1) * HW));
+        if (copy_off || (fp && off_out)) P.a[k].off_out = const_cast<void *>(at(off_out, b0 * 2 * (K + 1) * HW));
+        if (fp) {  // the prologue in the launch: raw inputs, conf' written here (read back by the rim staging)
+            P.a[k].flags |= kResFirst;
+            P.a[k].conf = at(fp->conf_out, b0 * HW);
+            P.a[k].aff = at(fp->aff_raw, b0 * fp->aff_bs);
+            P.a[k].aff_bs = fp->aff_bs;
+            P.a[k].pinit = at(fp->pinit, b0 * HW);
+            P.a[k].conf_raw = at(fp->conf_raw, b0 * HW);
+            P.a[k].gamma = fp->gamma;
+            P.a[k].kind = fp->kind;
+            P.a[k].aff_out = const_cast<void *>(at(fp->aff_out, b0 * (K + 1) * HW));
+        }
     }
     // The full image groups run in turn inside ONE launch (ResArgs::ngroups): no launch
     // boundary between them, so a part sets up its next group while others finish the
@@ -503,7 +542,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const char *menv = getenv("NLSPN_RES_MERGE");
     const int nfull = B / S.Bg;
     if (dbg & 8u) {  // trace stamps (experiments build) go into pred: each launch's part must hold them
-        const long long per = (long long)T * (kResWTrace ? 29 : 5) * 8;
+        const long long per = (long long)(T + 1) * (kResWTrace ? 29 : 5) * 8;  // rows: the setup, then one per iteration
         for (int k = 0; k < ng; ++k)
             if ((long long)(B - (long long)k * S.Bg) * HW * (long long)es < (long long)P.grid[k] * per) {
                 P.err = fail(NLSPN_EINVAL, "resident trace (NLSPN_RES_DBG=8): pred holds %lld bytes from image group %d, "
@@ -515,7 +554,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
         P.a[0].ngroups = nfull;
         // the group-loop build for the merged launch; a partial last group keeps the other
-        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true, pitch_ok, tail) : res_fn<__half>(S.nt, true, pitch_ok, false);
+        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true, pitch_ok, tail, P.first)
+                                               : res_fn<__half>(S.nt, true, pitch_ok, false, P.first);
         int n = 1;
         if (ng > nfull) {  // the partial group, launched after the merged one
             P.a[1] = P.a[ng - 1];
@@ -626,9 +666,11 @@ unsigned elementwise_grid(long long groups) {
 }
 
 // The whole section (see nlspn_propagate).  ev (optional, 2*T events): a dispatch-
-// recorded pair around each launch — [0,1] step 1, then [2,3] the resident kernel
-// or [2t, 2t+1] per-iteration step t+1.  *resident (optional): 1 if the resident
-// kernel ran iterations 2..T.
+// recorded pair around each launch — [0,1] step 1 (an empty interval when the resident
+// launches run the prologue), then [2,3] the resident kernel or [2t, 2t+1] per-iteration
+// step t+1.  *resident (optional): the resident launches' count if the resident kernel
+// ran iterations 2..T, | kResidentFirstBit if it also ran the prologue and iteration 1.
+constexpr int kResidentFirstBit = 0x100;  // (bench.py RESIDENT_FIRST)
 int propagate_impl(int dtype, const void *pred_init, const void *dep, const void *conf, const void *aff_raw,
                    int64_t aff_bstride, const void *off_raw, int64_t off_bstride, const float *gamma,
                    void *pred_inter, void *pred, void *aff_out, void *off_out, void *conf_out, void *workspace,
@@ -675,9 +717,26 @@ int propagate_impl(int dtype, const void *pred_init, const void *dep, const void
 
     if (resident) *resident = 0;
     ResPlan P;
+    // the prologue and iteration 1 inside the resident launches (no step-1 launch) where the
+    // resident kernel applies; NLSPN_RES_FIRST=0 (A/B) keeps step 1 in front of them
+    const char *fenv = getenv("NLSPN_RES_FIRST");
+    const ResFirst F{pred_init, conf, aff_raw, (long long)aff_bstride, gamma, kind, aff_out, conf ? conf_out : nullptr};
     const bool res = plan_resident(dtype, conf ? conf_out : nullptr, dep, aff_out, off_raw, off_bstride, pred_inter,
-                                   pred, workspace, B, H, W, kh, kw, T, flags, P, off_out);
+                                   pred, workspace, B, H, W, kh, kw, T, flags, P, off_out,
+                                   fenv && fenv[0] == '0' ? nullptr : &F);
     if (P.err) return P.err;
+    if (res && P.first) {
+        // The resident kernel's sync words start every launch at zero and every launch leaves
+        // them zero (res_finish); a plan clears its workspace once at creation, a direct call
+        // clears it here (the caller's workspace may hold anything)
+        if (!g_rec) NLSPN_HIP_TRY(hipMemsetAsync(workspace, 0, P.sync_bytes, s));
+        if (ev) {  // no step 1: an empty interval
+            NLSPN_HIP_TRY(hipEventRecord(ev[0], s));
+            NLSPN_HIP_TRY(hipEventRecord(ev[1], s));
+        }
+        if (resident) *resident = P.ngroups | kResidentFirstBit;
+        return launch_resident(P, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    }
     if (res && P.a[0].off_out) r1.a.off_out = nullptr;  // the resident loop copies the offsets
     if (res) {  // step 1 zeroes the resident kernel's sync words and poisons plane 1 (its hand-off)
         r1.a.zero_words = P.a[0].sync;
@@ -973,6 +1032,9 @@ int nlspn_plan_create(nlspn_plan_t *plan, int dtype, const void *pred_init, cons
     if (!plan) return fail(NLSPN_EINVAL, "plan is null");
     *plan = nullptr;
     (void)dev_state();  // its one-time host allocation must not happen inside the capture
+    // the resident kernel's sync words: zero before the plan's first launch (each launch leaves
+    // them so); outside the capture
+    if (workspace) NLSPN_HIP_TRY(hipMemset(workspace, 0, kSyncBytes));
     hipStream_t cs = nullptr;
     NLSPN_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);

@@ -9,16 +9,19 @@ namespace nlspn {
 // 576; one NYU image, C1: 128), so the LDS row addresses fold into immediates;
 // 0 = any other shape (thread count read at run time).  GROUPS = true: several image
 // groups in turn in one launch (C3 KITTI B=4: 576 threads; others: run-time count).
-#define NLSPN_RES_INST(T)                                                                \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false>(ResArgs);   \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true>(ResArgs);    \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true>(ResArgs);
-NLSPN_RES_INST(float)
-NLSPN_RES_INST(__half)
+#define NLSPN_RES_INST(T, F)                                                                \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>(ResArgs);    \
+    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
+// F: the forward prologue and iteration 1 inside the launch (ResArgs kResFirst), or after step 1
+NLSPN_RES_INST(float, true)
+NLSPN_RES_INST(__half, true)
+NLSPN_RES_INST(float, false)
+NLSPN_RES_INST(__half, false)
 // the eight-wave build (kResTailNT: affinities in VGPRs, tail pixels; fp32), launch bound 512
 // (two waves per SIMD: 256 VGPRs per lane)
-template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false>(ResArgs);
-template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true>(ResArgs);
+template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
+template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 }  // namespace nlspn

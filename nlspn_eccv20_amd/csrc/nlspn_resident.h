@@ -97,6 +97,20 @@ struct ResArgs {
     // planes, one output plane per iteration, so the copy rides the latency-bound loop instead
     // of step 1's HBM-bound pass (raw offset layout only).
     void *off_out;
+    // The forward prologue inside the launch (flags kResFirst, round 5): no step-1 launch.  The
+    // setup reads the RAW head outputs — `aff` then holds K raw affinity planes per item at
+    // batch stride aff_bs, `conf_raw` the raw confidence, `pinit` pred_init — normalises the
+    // affinities itself (_affinity_normalization + _aff_insert, nlspnmodel.py:179-201, 261-269),
+    // builds conf' (:328-334) and stores it to `conf` (conf_out, the output dict's confidence and
+    // the rim staging's conf' source), and iteration 1 runs as the loop's t = 0 from
+    // f0 = p0 * conf' of the raw inputs (:341-348).  The output dict's normalised affinity is
+    // written to `aff_out` by the loop, one plane per iteration, like off_out.
+    const void *pinit;
+    const void *conf_raw;
+    const float *gamma;
+    void *aff_out;
+    long long aff_bs;
+    int kind;
 };
 
 typedef const __attribute__((address_space(4))) ResArgs ResArgsK;  // the kernarg segment's ResArgs
@@ -109,7 +123,11 @@ constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per
 #ifndef NLSPN_RES_TAIL_SMAX
 #define NLSPN_RES_TAIL_SMAX 1
 #endif
-constexpr int kResTailSMax = NLSPN_RES_TAIL_SMAX;  // the same, eight-wave build (A/B builds: 2, 3)
+constexpr int kResTailSMax = NLSPN_RES_TAIL_SMAX;
+#ifndef NLSPN_RES_PRE
+#define NLSPN_RES_PRE 2
+#endif
+constexpr int kResPre = NLSPN_RES_PRE;  // the prologue's window staging: quads per thread in flight  // the same, eight-wave build (A/B builds: 2, 3)
 #ifndef NLSPN_RES_PF
 #define NLSPN_RES_PF 0
 #endif
@@ -181,9 +199,13 @@ constexpr bool kResGeneralPath = false;  // experiment only: wrong results for t
 constexpr unsigned kSc1 = 16u;                   // buffer-instruction aux bit: sc1 (write-through / L1 bypass)
 constexpr unsigned kResOffInserted = 0x100u;      // ResArgs::flags: offsets in the inserted 2(K+1)-plane layout
 constexpr unsigned kResL2 = 0x400u;               // ResArgs::flags: same-XCD hand-offs may stay in the XCD's L2
-// The sync workspace: one 128-B line per word group — [0] the abort word, then per part
-// i (blockIdx) the line kResLine * (1 + i) holding (word + 1) its tagged XCC id.  No two
-// parts share a line, so a line is only ever written from one XCD.
+constexpr unsigned kResFirst = 0x800u;            // ResArgs::flags: the prologue and iteration 1 in the launch
+// The sync workspace: one 128-B line per word group — [0] the abort word, [1] the count of
+// parts that have finished, then per part i (blockIdx) the line kResLine * (1 + i) holding
+// (word + 1) its tagged XCC id.  No two parts share a line, so a line is only ever written
+// from one XCD.  The words are zero when a launch starts and zero again when it ends: the
+// last part to finish (the count) clears them (res_finish), so a plan's launches need no
+// clearing pass (the host clears a workspace once, before its first resident launch).
 constexpr int kResLine = 32;
 // "not yet written" values of the handed-off planes (nlspn_step.h kPoison32 / kPoison16,
 // also stored by step 1): signalling NaNs (quiet bit clear), which no arithmetic result is
@@ -217,11 +239,27 @@ __device__ __forceinline__ void res_span_merge(int *ctl, bool on, int mn, int mx
     }
 }
 
+// A part's exit, once every wave of it has made its last read of the sync words (the
+// caller's barrier): one add to the finished-parts count; the part whose add completes the
+// grid zeroes the abort word, the count and every part's XCC-id word for the next launch
+// (every other part has made its last read before its own add).  Wave 0 only.
+__device__ __forceinline__ void res_finish(gu32 *sync) {
+    if (threadIdx.x >= 64) return;
+    unsigned done = 0;
+    if (threadIdx.x == 0) done = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done != gridDim.x - 1) return;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += 64)
+        __hip_atomic_store(&sync[kResLine * (1 + i) + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 2) __hip_atomic_store(&sync[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The trace's per-wave stamp pair of iteration t (dbg 8): after every part's five stamps
-// per iteration, 12 pairs per part and iteration; wb = the wave's first thread (uniform)
+// per row (T + 1 rows: the setup, then iteration t in row t + 1), 12 pairs per part and row;
+// wb = the wave's first thread (uniform); t = -1: row 0 (the wave's HW_ID)
 __device__ __forceinline__ unsigned long long *res_wtrace(void *pred, int T, unsigned wb, int t) {
-    return reinterpret_cast<unsigned long long *>(pred) + (size_t)gridDim.x * T * 5 +
-           ((size_t)blockIdx.x * T + t) * 24 + 2 * (wb >> 6);
+    return reinterpret_cast<unsigned long long *>(pred) + (size_t)gridDim.x * (T + 1) * 5 +
+           ((size_t)blockIdx.x * (T + 1) + t + 1) * 24 + 2 * (wb >> 6);
 }
 
 // A value as storage type T holds it (fp32: itself; fp16: rounded), back in fp32.
@@ -340,7 +378,7 @@ template <> struct ResVec<__half> {
 // NTC = kResTailNT (512): the eight-wave build (affinities in VGPRs, tail pixels).
 // GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
 // folds away, and with it the setup spill slots it costs).
-template <typename T, int MAXNT, int SMAX, int NTC, bool GROUPS>
+template <typename T, int MAXNT, int SMAX, int NTC, bool GROUPS, bool FIRST>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RXQ = kResRXQ, PADX = kResPadX;
     constexpr unsigned ES = sizeof(T);
@@ -413,7 +451,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // expression (.cuh:178-179), so the geometry below starts from them.
     // trace (dbg 8): row t = 0 of this part holds the setup stamps
     unsigned long long *trace0 = (exp_dbg(a.dbg) & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
-                                                   (size_t)blockIdx.x * a.T * 5 : nullptr;
+                                                   (size_t)blockIdx.x * (a.T + 1) * 5 : nullptr;
     if (trace0 && tid == 0) trace0[0] = __builtin_amdgcn_s_memrealtime();
     // trace: per wave and iteration two more stamps (taps + stores issued, stores drained)
     // after the parts' five, 24 per part and iteration (wave-uniform addresses, res_wtrace);
@@ -421,29 +459,32 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     if (kResWTrace && trace0 && (threadIdx.x & 63) == 0) {
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        res_wtrace(a.pred, a.T, __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u), 0)[0] = hw;
+        res_wtrace(a.pred, a.T, __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u), -1)[0] = hw;
     }
     // TAIL: the threads own the part's first NT quads as quads, the rest as tail pixels (below)
     const int nq_main = TAIL ? min(nown, NT) : nown;
     const bool active = tid < nq_main;
-    // Same-XCD hand-offs (flags kResL2, host: plane layout line-aligned): every
-    // part publishes the XCC it runs on; if all parts of its image share one, the image's
-    // hand-offs stay in that XCD's L2 (below).  Placement is read, never assumed: the word
-    // is tagged with this launch (its epoch + 1, above the 5-bit XCC field), and a reader
-    // waits for THIS launch's tag, so a second launch of a section (a partial last group,
-    // unmerged groups, trace mode) never decides from the previous launch's placement.
-    // The words are zeroed once per section (step 1), and a section's launches have
-    // distinct epochs.
+    // Every part publishes, once its setup is done, the XCC it runs on, tagged with the image
+    // group (grp + 1, above the 5-bit XCC field; the words start every launch at zero,
+    // res_finish), and iteration 1 of the group waits until every part of its image has
+    // published a tag of this group or a later one.  Two uses:
+    //  * same-XCD hand-offs (flags kResL2, host: plane layout line-aligned): if all parts of
+    //    the image share one XCC, the image's hand-offs stay in that XCD's L2 (below).
+    //    Placement is read, never assumed;
+    //  * the prologue in the launch (kResFirst): a part publishes only after its stores of
+    //    conf' and of plane 0's poison are acknowledged, so a consumer that has seen every tag
+    //    of its image reads neither a previous call's conf' nor its plane 0 (the sc1 row of
+    //    MI355X_MICROARCH.md's hand-off table: sc1 stores, every storing wave's vmcnt(0) and a
+    //    workgroup barrier before the tag, sc1 loads behind the poll and a barrier).
     const bool l2try = (a.flags & kResL2) != 0;
+    constexpr bool first = FIRST && !TAIL;  // (the eight-wave build: no prologue form)
+    const bool publish = l2try || first;
     unsigned xcc_self = 0;
-    const unsigned xtag = (a.epoch + 1u) << 5;
-    if (l2try) {
+    const unsigned xtag = (unsigned)(grp + 1) << 5;
+    if (publish) {
         unsigned x;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
         xcc_self = (x & 0xfu) + 1u;
-        if (grp == 0 && tid == 0)
-            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
     }
     const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
@@ -475,11 +516,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     {
         float dv[4];
         float ak[K][4], aref[4];
-        const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
+        // the normalised (K+1)-plane layout, or with the prologue in the launch the K raw planes
+        const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (first ? (long long)b * a.aff_bs : (long long)b * (K + 1) * HW));
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes, ak[k]);
+            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(first || k < REF ? k : k + 1) * plane_bytes, ak[k]);
             const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
@@ -488,13 +530,39 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         for (int e = 0; e < 4; ++e) dv[e] = 0.f;
         if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
         float cq[4] = {1.f, 1.f, 1.f, 1.f};
-        if (has_conf) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), vpix, 0u, cq);
+        if (has_conf)
+            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(first ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
+        if (first) {
+            // the prologue (step 1's FIRST path, the same IEEE sequence): conf' = (1 - m) conf + m,
+            // m = dep > 0 (:328-334), stored (the output dict's confidence, and the conf' other
+            // parts stage from); plane 0 poisoned (iteration 1 of the launch reads it from the
+            // other parts).  The affinities are normalised below, from the LDS rows.
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
-            float s = 0.f;
+            for (int e = 0; e < 4; ++e) aref[e] = 0.f;
+            if (preserve) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) s += ak[k][e];
-            aref[e] = 1.0f - s;
+                for (int e = 0; e < 4; ++e) {
+                    const float m = dv[e] > 0.f ? 1.f : 0.f;
+                    cq[e] = (1.0f - m) * cq[e] + m;
+                }
+            }
+            if (active) {
+                if (has_conf) ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(const_cast<void *>(a.conf)) + b * HW), vpix, 0u, cq);
+                ResVec<T>::template poison<kSc1>(make_rsrc(static_cast<T *>(a.pred_inter) + b * HW), vpix);
+            }
+            // conf' as stored (fp16: rounded): the own quad's f_t = p_t * conf' of every later
+            // iteration uses it, as the staging's loads of the stored planes do (iteration 1
+            // stages f0 from the unrounded value, as step 1 does)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cq[e] = round_to<T>(cq[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < K; ++k) s += ak[k][e];
+                aref[e] = 1.0f - s;
+            }
         }
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
@@ -529,6 +597,26 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             taf[K + 2] = preserve ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), tvpix, 0u) : 0.f;
 #pragma unroll
             for (int k = 0; k < K + 3; ++k) tal[256 * k] = taf[k];
+        }
+    }
+    // the prologue: the affinity normalisation with the reference-tap weight 1 - sum
+    // (nlspn_common.h normalize_taps, step 1's IEEE sequence), one pixel of the quad at a time
+    // from the raw values in the LDS rows (a rolled loop: the 4 x K values of the quad at once
+    // cost the GROUPS builds scratch)
+    if constexpr (!TAIL) {
+        if (first) {
+            const float gamma = *a.gamma;
+#pragma unroll 1
+            for (int e = 0; e < 4; ++e) {
+                float *row = reinterpret_cast<float *>(akl) + e;
+                float t1[K][1], r1[1];
+#pragma unroll
+                for (int k = 0; k < K; ++k) t1[k][0] = row[4 * k];
+                normalize_taps<K, 1>(t1, r1, a.kind, gamma);
+#pragma unroll
+                for (int k = 0; k < K; ++k) row[4 * k] = t1[k][0];
+                row[4 * K] = r1[0];
+            }
         }
     }
     // the quad's row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
@@ -612,7 +700,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int ra = max(rlo, 0), rb = min(rhi, H - 1);      // in-image window rows
     const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
     const int wqn = qb - qa + 1;
+    // (the prologue's conf' and poison stores acknowledged by every wave before the barrier
+    // behind which the part publishes: issued before the window pass, so nothing is left)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    if (publish && tid == 0)
+        __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     lds_barrier();
@@ -753,23 +847,67 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             c = cc < left ? qa + cc : c1 + cc - left;
         }
     };
-    // Iteration t (1 .. T-1: the section's iterations 2 .. T) reads plane t-1 and writes
-    // plane t.  Plane 0 is step 1's output (the launch's input: never poisoned), so the
-    // first iteration stages without waiting.  The XCC ids are read by the last wave holding
-    // quads (any wave would do).
+    // ---- the prologue in the launch: iteration 1 (the loop's t = 0) stages the whole in-image
+    // window from the raw inputs, f0 = p0 * conf' with p0 = (1 - m) pred_init + m dep
+    // [clamped] and the unrounded conf' (step 1's make_f, :328-348), by plain loads: none of
+    // these planes is written by the launch.  Up to kResPre quads per thread in flight.
+    if (first) {
+        const T *pin = static_cast<const T *>(a.pinit) + b * HW;
+        const rsrc_t rpi = make_rsrc(pin);
+        const rsrc_t rcr = make_rsrc(has_conf ? static_cast<const T *>(a.conf_raw) + b * HW : pin);
+        const rsrc_t rdr = make_rsrc(preserve ? static_cast<const T *>(a.dep) + b * HW : pin);
+        bool nonfin = false;
+        for (int base = tid; base < nall; base += kResPre * NT) {
+            float pv[kResPre][4], cv[kResPre][4], dv[kResPre][4];
+            int li[kResPre];
+#pragma unroll
+            for (int s = 0; s < kResPre; ++s) {
+                const int k = base + s * NT, rr = res_div(k, wqn, rwqn), r = ra + rr, c = qa + k - rr * wqn;
+                li[s] = (r - rlo) * WW + 4 * (c - wq0) + PADX;
+                const unsigned q = (unsigned)(r * W + 4 * c) * ES;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { cv[s][e] = 1.f; dv[s][e] = 0.f; }
+                if (k < nall) {
+                    ResVec<T>::template load<0>(rpi, q, 0u, pv[s]);
+                    if (has_conf) ResVec<T>::template load<0>(rcr, q, 0u, cv[s]);
+                    if (preserve) ResVec<T>::template load<0>(rdr, q, 0u, dv[s]);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < kResPre; ++s) {
+                if (base + s * NT >= nall) continue;
+                float f[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) f[e] = make_f<true>(pv[s][e], cv[s][e], dv[s][e], has_conf, preserve, clip);
+                nonfin |= !__builtin_isfinite((f[0] + f[1]) + (f[2] + f[3]));
+                *reinterpret_cast<float4 *>(&fwin[li[s]]) = make_float4(f[0], f[1], f[2], f[3]);
+                fwinB[li[s] - 1] = f[0];
+                *reinterpret_cast<float2 *>(&fwinB[li[s]]) = make_float2(f[1], f[2]);
+                fwinB[li[s] + 2] = f[3];
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(nonfin) != 0 && lane == 0) ctl[6] = 1;  // iteration 0's flag
+    }
+
+    // Iteration t reads plane t-1 and writes plane t: t = 1 .. T-1 (the section's iterations
+    // 2 .. T) after step 1, whose plane 0 is the launch's input (never poisoned: the first
+    // iteration stages without waiting); with the prologue in the launch t = 0 .. T-1, t = 0
+    // staged above.  The XCC ids are read by the last wave holding quads (any wave would do).
+    const int t0 = first ? 0 : 1;
     const int pwave = (nq_main - 1) >> 6;
-    bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in the first iteration)
+    bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in iteration 1)
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     int t_abort = 0;
-    for (int t = 1; t < a.T; ++t) {
+    for (int t = t0; t < a.T; ++t) {
+        // trace rows: 0 the setup, t + 1 iteration t
         unsigned long long *trace = (exp_dbg(a.dbg) & 8u) ? reinterpret_cast<unsigned long long *>(a.pred) +
-                                                       ((size_t)blockIdx.x * a.T + t) * 5 : nullptr;
+                                                       ((size_t)blockIdx.x * (a.T + 1) + t + 1) * 5 : nullptr;
         if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
-        const rsrc_t rp = make_rsrc(p_all + (size_t)(t - 1) * a.tstride + b * HW);
-        // ---- the inserted-offset copy (ResArgs::off_out): output plane t - 1 (a raw plane, or
+        const rsrc_t rp = make_rsrc(p_all + (size_t)(t > 0 ? t - 1 : 0) * a.tstride + b * HW);
+        // ---- the inserted-offset copy (ResArgs::off_out): output plane t - t0 (a raw plane, or
         // the reference tap's zero plane) loaded here, stored after the staging phase (by then
         // the staging waits have covered the load)
-        const int cpc = t - 1;
+        const int cpc = t - t0;
         const bool cpy = a.off_out != nullptr && cpc < 2 * (K + 1);
         const int cptt = cpc >> 1;
         const int cpsrc = cptt == REF ? -1 : 2 * (cptt < REF ? cptt : cptt - 1) + (cpc & 1);
@@ -779,26 +917,39 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (active) ResVec<T>::template load<0>(ro, vpix, (unsigned)cpsrc * plane_bytes, cpq);
             if (tail_on) cpq1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)cpsrc * plane_bytes);
         }
-        // ---- a launch's first iteration: the hand-off mode of this image (all its parts
-        // on this part's XCC: L2), decided from the published XCC ids, identically by
-        // every part of the image; its stores use it
+        // ---- iteration 1, the first to read other parts' cells: wait until every part of the
+        // image has published this group's tag (or a later group's); then the hand-off mode of
+        // this image (all its parts on this part's XCC: L2), decided from the published XCC
+        // ids, identically by every part of the image; its stores use it.  With the prologue
+        // in the launch a timed-out wait aborts (the conf' and plane 0 it guards are unknown).
         if (t == 1) {
             if ((tid >> 6) == pwave) {
                 bool same = l2try, fail = false;
                 unsigned spins = 0;
-                for (int base = 0; base < nparts && same && !fail; base += 64) {
+                for (int base = 0; publish && base < nparts && !fail; base += 64) {
                     const int jj = base + lane;
                     gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
                     unsigned v;
                     for (;;) {
                         v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (__all((v & ~31u) == xtag)) break;
-                        if (++spins > kResSpinLimit) { fail = true; break; }
+                        if (__all((v >> 5) >= (xtag >> 5))) break;
+                        if (++spins > kResSpinLimit ||
+                            ((spins & 15u) == 0u && __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+                            fail = true;
+                            break;
+                        }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    same = same && __all(v == (xtag | xcc_self));
+                    same = same && __all((v & 31u) == xcc_self);
                 }
-                if (lane == 0) ctl[5] = same && !fail ? 1 : 0;
+                if (lane == 0) {
+                    ctl[5] = same && !fail ? 1 : 0;
+                    if (fail && first) {
+                        ctl[0] = 1;
+                        __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
             }
             lds_barrier();
             l2 = __builtin_amdgcn_readfirstlane(ctl[5]) != 0;
@@ -809,12 +960,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // re-loaded until not the poison (written by other parts in this launch), conf' by
         // plain loads (invariant).  After a launch's first iteration the own quads are in the
         // window already (written back below), so only the other parts' quads are loaded.
-        const bool rim = t > 1;
+        const bool rim = t > t0;
         const bool spin = rim && !(exp_dbg(a.dbg) & 1u);
         // the staging index (= tid) rebuilt per iteration from the wave's base (an SGPR) and
         // the lane id, so no VGPR holds it across the loop (it was spilled and reloaded)
         const int tb = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        const int nsq_it = (exp_dbg(a.dbg) & 2u) ? 0 : (rim ? nrest : nall);
+        // (the prologue's t = 0: staged from the raw inputs above)
+        const int nsq_it = (exp_dbg(a.dbg) & 2u) ? 0 : (rim ? nrest : (first ? 0 : nall));
         bool nonfin = false;  // this thread staged a non-finite f
         for (int base = tb; base < nsq_it; base += SM * NT) {
             float sv[SM][4], cv[SM][4];
@@ -836,7 +988,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 gq[s] = (unsigned)(r * W + 4 * c) * ES;
                 if (k < nsq_it) {
                     ok = ResVec<T>::template load_p<kSc1>(rp, gq[s], sv[s]) && ok;
-                    if (has_conf) ResVec<T>::template load<0>(rcg, gq[s], 0u, cv[s]);
+                    // conf': sc1 when this launch wrote it (the prologue's setup, published by the tags)
+                    if (has_conf) {
+                        if (first) ResVec<T>::template load<kSc1>(rcg, gq[s], 0u, cv[s]);
+                        else ResVec<T>::template load<0>(rcg, gq[s], 0u, cv[s]);
+                    }
                 }
             }
             if (spin) {  // this wave's lanes re-load the quads still poisoned (a bounded spin)
@@ -893,7 +1049,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)cpc * plane_bytes, cpq1);
             if (t == a.T - 1) {  // a short section: the planes past T - 1, here
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
-                for (int c = t; c < 2 * (K + 1); ++c) {
+                for (int c = cpc + 1; c < 2 * (K + 1); ++c) {
                     const int tt = c >> 1, src = tt == REF ? -1 : 2 * (tt < REF ? tt : tt - 1) + (c & 1);
                     float q[4] = {0.f, 0.f, 0.f, 0.f}, q1 = 0.f;
                     if (src >= 0) {
@@ -903,6 +1059,25 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     if (active) ResVec<T>::template store<kNT>(rco, vpix, (unsigned)c * plane_bytes, q);
                     if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)c * plane_bytes, q1);
                 }
+            }
+        }
+        // the prologue's normalised affinity (the output dict's `aff`, (K+1) planes), from the
+        // quad's rows, streamed one plane per iteration: plane 0 and the reference tap's plane K/2
+        // (1 - sum as the normalisation left it) in iteration 0, plane t in iteration t, the rest
+        // in the last iteration of a short section
+        if constexpr (!TAIL) {
+            if (first && active && (t <= K || t == a.T - 1)) {
+                const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + (long long)b * (K + 1) * HW);
+                const auto put = [&](const int c) {
+                    const float4 v = akl[c == REF ? K : (c < REF ? c : c - 1)];
+                    const float q[4] = {v.x, v.y, v.z, v.w};
+                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, q);
+                };
+                if (t == 0) put(REF);
+                if (t != REF && t <= K) put(t);
+                if (t == a.T - 1)
+                    for (int c = t + 1; c <= K; ++c)
+                        if (c != REF) put(c);
             }
         }
         // the window holds a non-finite f (staged now, or an own quad written back after
@@ -1004,7 +1179,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                     }
                                     __builtin_amdgcn_s_sleep(1);
                                 }
-                                c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                                c4[u] = has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
                             }
                         }
                         v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
@@ -1182,7 +1357,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                                 }
                                                 __builtin_amdgcn_s_sleep(1);
                                             }
-                                            c4[u] = has_conf ? pv * ResVec<T>::template load1<0>(rcg, qo, 0u) : pv;
+                                            c4[u] = has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
                                         }
                                     }
                                     v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
@@ -1293,6 +1468,22 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             fwinB[town - 1] = f;
             if (!__builtin_isfinite(f)) ctl[6 + ((t + 1) & 1)] = 1;
         }
+        // fp16 storage with the prologue in the launch: iteration 1 used the normalisation's
+        // own values (step 1 does); later iterations use them as stored, as the step launches
+        // read them back (rounded to fp16, the reference-tap weight 1 - sum of the rounded ones)
+        if constexpr (!TAIL && ES == 2) {
+            if (first && t == t0) {
+                float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    float4 v = akl[k];
+                    v.x = round_to<T>(v.x); v.y = round_to<T>(v.y); v.z = round_to<T>(v.z); v.w = round_to<T>(v.w);
+                    akl[k] = v;
+                    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
+                }
+                akl[K] = make_float4(1.0f - s4[0], 1.0f - s4[1], 1.0f - s4[2], 1.0f - s4[3]);
+            }
+        }
     }
     // aborted: NaN in every plane this part has not written (this group's remaining
     // iterations, every later group's), then exit.  Write-through: a consumer spinning on
@@ -1303,7 +1494,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
             for (int g2 = grp; g2 < ngroups; ++g2) {
                 const int b2 = bl + g2 * a.B;
-                for (int tt = g2 == grp ? t_abort : 1; tt < a.T; ++tt)
+                for (int tt = g2 == grp ? t_abort : t0; tt < a.T; ++tt)
                     ResVec<T>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
                 ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
             }
@@ -1311,16 +1502,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (tail_on) {
             for (int g2 = grp; g2 < ngroups; ++g2) {
                 const int b2 = bl + g2 * a.B;
-                for (int tt = g2 == grp ? t_abort : 1; tt < a.T; ++tt)
+                for (int tt = g2 == grp ? t_abort : t0; tt < a.T; ++tt)
                     ResVec<T>::template store1<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), tvpix, 0u,
                                                      __builtin_nanf(""));
                 ResVec<T>::template store1<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), tvpix, 0u, __builtin_nanf(""));
             }
         }
+        lds_barrier();  // (every wave of the part is here: the abort word is read after a barrier)
+        res_finish(sync);
         return;
     }
     if (!GROUPS || grp + 1 >= ngroups) break;
     }  // image groups
+    lds_barrier();  // every wave has made its last read of the sync words
+    res_finish(sync);
 }
 
 }  // namespace nlspn

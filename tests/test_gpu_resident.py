@@ -1,6 +1,6 @@
-"""GPU: the resident propagation kernel (iterations 2..T in one launch per image
-group after a step-1 launch, invariant planes on chip, poisoned-plane hand-offs)
-against the per-iteration launches and the oracle.
+"""GPU: the resident propagation kernel (the prologue and iterations 1..T in one launch
+per image group — or iterations 2..T after a step-1 launch, NLSPN_RES_FIRST=0 — invariant
+planes on chip, poisoned-plane hand-offs) against the per-iteration launches and the oracle.
 
 Bar: BIT-EXACT against step 1 + the T-1 per-iteration launches (all forms issue the
 same IEEE sequence per pixel; only the schedule and the hand-off differ), every one
@@ -63,10 +63,13 @@ def _nan_equal(x, y):
 
 
 def _both(inp, T=18, nan_ok=False, **kw):
-    """(resident, steps): the default resident form (behind a step-1 launch), checked
-    here against the resident form with every hand-off write-through (NLSPN_RES_L2=0: no
-    image's hand-offs kept in an XCD's L2) and against the nine-wave build where the
-    eight-wave one applies (NLSPN_RES_TAIL), and the step form.
+    """(resident, steps): the default resident form (since round 5 the prologue and
+    iteration 1 inside the resident launches, no step-1 launch), checked here against the
+    resident form behind a step-1 launch (NLSPN_RES_FIRST=0), with every hand-off
+    write-through (NLSPN_RES_L2=0: no image's hand-offs kept in an XCD's L2), against the
+    other of the eight- and nine-wave builds where the eight-wave one applies
+    (NLSPN_RES_TAIL; the eight-wave build runs behind step 1), and the step form — every
+    pred_inter plane, pred and the prologue's output-dict tensors.
     nan_ok: NaN results compare by position (_nan_equal)."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
@@ -75,6 +78,8 @@ def _both(inp, T=18, nan_ok=False, **kw):
         # the other of the eight- and nine-wave builds where the eight-wave one applies
         with _env("0" if _lib_tail_default() else "1", "NLSPN_RES_TAIL"):
             d = propagate(*inp, prop_time=T, **kw)
+        with _env("0", "NLSPN_RES_FIRST"):
+            f = propagate(*inp, prop_time=T, **kw)
     with _env("0"):
         b = propagate(*inp, prop_time=T, **kw)
     torch.cuda.synchronize()
@@ -82,11 +87,15 @@ def _both(inp, T=18, nan_ok=False, **kw):
         if a[k] is not None or b[k] is not None:
             assert _bits_equal(a[k], b[k]), k
             assert _bits_equal(c[k], b[k]), k
+            assert _bits_equal(d[k], b[k]), k
+            assert _bits_equal(f[k], b[k]), k
     eq = _nan_equal if nan_ok else _bits_equal
     assert eq(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
     assert eq(a["pred"], c["pred"])
     assert eq(a["pred_inter_tensor"], d["pred_inter_tensor"]), "eight-wave and nine-wave builds differ"
     assert eq(a["pred"], d["pred"])
+    assert eq(a["pred_inter_tensor"], f["pred_inter_tensor"]), "prologue in the launch and step 1 differ"
+    assert eq(a["pred"], f["pred"])
     return a, b
 
 
@@ -299,7 +308,11 @@ def test_time_propagate_reports_resident():
     with _env("1"):
         plan = PropagationPlan(*inp, prop_time=18)
         first, rest, res = timed(plan.outputs)
-        assert res == 1 and first > 0 and rest > 0  # one resident launch (one image group) behind step 1
+        # one resident launch (one image group) with the prologue inside (0x100): no step 1
+        assert res == 0x101 and first >= 0 and first < 0.01 and rest > 0
+        with _env("0", "NLSPN_RES_FIRST"):
+            first, rest, res = timed(plan.outputs)
+        assert res == 1 and first > 0 and rest > 0  # behind step 1
         plan.close()
 
 

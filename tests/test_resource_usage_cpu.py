@@ -7,6 +7,7 @@ not hide in the build log.  If the library has not been built here, the resident
 translation unit (seconds) is compiled with the remarks on the spot.
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -25,13 +26,17 @@ HOT = ("prop_step_kernel", "bwd_step_kernel", "s2d_pyramid_kernel")
 # launch) wrap the iteration loop in the group loop, so it sits at depth 2.  The loop is
 # also checked on the kernel's device assembly: no scratch instruction inside it.
 RESIDENT_SCRATCH_CAP = 0          # bytes per lane, single-group builds
-RESIDENT_SCRATCH_CAP_GROUPS = 16  # bytes per lane, GROUPS builds (setup slots of the fp16 one)
+# bytes per lane, GROUPS builds: setup spill slots only (the loop check below holds them out of
+# the iteration loop); round 5's prologue-in-the-launch builds (FIRST) spill 68-84 B around
+# their setup at the 168-VGPR cap
+RESIDENT_SCRATCH_CAP_GROUPS = 96
 RESIDENT_LOOP_RELOADS = 0         # scratch instructions inside the iteration loop, per instantiation
 RESIDENT_LOOP_RELOADS_F16 = 0     # the fp16 builds alike
 
 
 def _groups(name):
-    return "ELb1E" in name
+    # template <T, MAXNT, SMAX, NTC, GROUPS, FIRST>: GROUPS is the first of the two bools
+    return re.search(r"ELb1ELb[01]EEEv", name) is not None
 
 
 _FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize"]

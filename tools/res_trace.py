@@ -52,14 +52,20 @@ def main(config="nyu", T=18, reps=5, bg=None, out=None):
     res = {}
     for grp in range(ng):
         o = grp * bg * HW // 2  # group k's stamps start at its own pred planes (int64 = 2 floats)
-        st = allst[o: o + G * T * 5].reshape(G, T, 5).astype(np.float64) / 100.0  # us
-        res[f"group{grp}"] = phases(st, G, B if ng == 1 else bg, g, T)
-        # per-wave stamps (after every part's five): [part, t, wave, (taps+stores issued, drained)]
-        if o + G * T * 29 <= allst.size:  # room for the per-wave stamps (small batches: not)
-            wv = allst[o + G * T * 5: o + G * T * 29].reshape(G, T, 12, 2)
-            s2 = allst[o: o + G * T * 5].reshape(G, T, 5)[:, :, 2]
+        R = T + 1  # rows per part: the setup, then iteration t in row t + 1
+        raw = allst[o: o + G * R * 5].reshape(G, R, 5)
+        # with the prologue in the launch iteration 0 (the section's iteration 1) has a row;
+        # after a step-1 launch the loop starts at t = 1 (row 1 stays empty)
+        it0 = 1 if (raw[:, 1, 0] != 0).any() else 2
+        st = raw.astype(np.float64) / 100.0  # us
+        res[f"group{grp}"] = phases(st, it0)
+        res[f"group{grp}"]["prologue_in_launch"] = it0 == 1
+        # per-wave stamps (after every part's five): [part, row, wave, (taps+stores issued, drained)]
+        if o + G * R * 29 <= allst.size:  # room for the per-wave stamps (small batches: not)
+            wv = allst[o + G * R * 5: o + G * R * 29].reshape(G, R, 12, 2)
+            s2 = raw[:, :, 2]
             if (wv[:, 0, :, 0] != 0).any():  # builds with per-wave stamps (NLSPN_RES_WTRACE=1)
-                res[f"group{grp}"]["waves"] = waves(s2, wv)
+                res[f"group{grp}"]["waves"] = waves(s2, wv, it0)
     line = json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res})
     if out:  # the JSON alone (the runtime's stderr lines never land in the file)
         with open(out, "w") as f:
@@ -67,13 +73,13 @@ def main(config="nyu", T=18, reps=5, bg=None, out=None):
     print(line)
 
 
-def phases(st, G, B, g, T):
-    st -= st[:, 0, 0].min()  # row t = 0: setup stamps (entry, invariants loaded, window zeroed, taps classified)
+def phases(st, it0):
+    st -= st[:, 0, 0].min()  # row 0: setup stamps (entry, invariants loaded, window zeroed, taps classified)
     su = st[:, 0, :]
     setup = {"entry_spread": su[:, 0].max() - su[:, 0].min(), "invariant_loads": np.median(su[:, 1] - su[:, 0]),
              "window": np.median(su[:, 2] - su[:, 1]), "classify": np.median(su[:, 3] - su[:, 2]),
-             "geometry_to_loop": np.median(st[:, 1, 0] - su[:, 3]), "first_loop_top_max": st[:, 1, 0].max()}
-    st = st[:, 1:, :]  # iterations 2..T
+             "geometry_to_loop": np.median(st[:, it0, 0] - su[:, 3]), "first_loop_top_max": st[:, it0, 0].max()}
+    st = st[:, it0:, :]  # the launch's iterations (1..T with the prologue in it, else 2..T)
     ph = {"wait": st[:, :, 1] - st[:, :, 0], "stage": st[:, :, 2] - st[:, :, 1], "taps+store": st[:, :, 3] - st[:, :, 2],
           "drain+barrier": st[:, :, 4] - st[:, :, 3]}
     ph["loop"] = st[:, 1:, 0] - st[:, :-1, 4]
@@ -86,13 +92,14 @@ def phases(st, G, B, g, T):
     return out
 
 
-def waves(s2, wv):
+def waves(s2, wv, it0):
     """Per wave of a part: the median time (us) from the part's taps start (S2, after the
     staging barrier) to the wave's taps + stores issued and to its stores drained, over
-    iterations 2..T, and the SIMD the wave ran on (HW_ID bits 5:4, recorded at entry)."""
+    the launch's iterations after its first, and the SIMD the wave ran on (HW_ID bits 5:4,
+    recorded at entry, row 0)."""
     hw = wv[:, 0, :, 0]
     nw = int(max(1, ((hw != 0).any(0)).sum()))
-    rel = (wv[:, 1:, :nw, :].astype(np.float64) - s2[:, 1:, None, None].astype(np.float64)) / 100.0
+    rel = (wv[:, it0 + 1:, :nw, :].astype(np.float64) - s2[:, it0 + 1:, None, None].astype(np.float64)) / 100.0
     return {"simd": [int(np.bincount(((hw[:, w] >> 4) & 3).astype(np.int64), minlength=4).argmax()) for w in range(nw)],
             "issued": [round(float(np.median(rel[:, :, w, 0])), 3) for w in range(nw)],
             "drained": [round(float(np.median(rel[:, :, w, 1])), 3) for w in range(nw)]}
