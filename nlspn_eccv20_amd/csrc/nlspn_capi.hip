@@ -477,6 +477,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
         S.win_cells = kResTailWC;
         fp = nullptr;  // (the eight-wave build has no prologue form: step 1 runs before it)
     }
+    // Parts of two waves (a B=1 NYU image in 247 parts of 72 quads, C1): the prologue's
+    // setup work (27 raw planes, the normalisation's tanh / divisions) runs on two waves per
+    // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
+    // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
+    if (S.nt <= 128) fp = nullptr;
     P.first = fp != nullptr;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded); the eight-wave build keeps

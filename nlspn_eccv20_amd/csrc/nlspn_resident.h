@@ -104,7 +104,7 @@ struct ResArgs {
     // builds conf' (:328-334) and stores it to `conf` (conf_out, the output dict's confidence and
     // the rim staging's conf' source), and iteration 1 runs as the loop's t = 0 from
     // f0 = p0 * conf' of the raw inputs (:341-348).  The output dict's normalised affinity is
-    // written to `aff_out` by the loop, one plane per iteration, like off_out.
+    // written to `aff_out` by the setup.
     const void *pinit;
     const void *conf_raw;
     const float *gamma;
@@ -513,32 +513,37 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     float hy[K][4], hx[K][4];
     float4 aq[K + 1];          // TAIL: the quad's affinities and 1 - sum (what akl holds otherwise)
     float thy[K] = {}, thx[K] = {};  // TAIL: the tail pixel's sample coordinates
+    // the quad's affinities, dep and conf (with the prologue in the launch: raw, processed after
+    // the geometry pass below, so that pass runs while they stream in)
+    float ak[K][4], dv[4], cq[4] = {1.f, 1.f, 1.f, 1.f};
     {
-        float dv[4];
-        float ak[K][4], aref[4];
+        float aref[4];
         // the normalised (K+1)-plane layout, or with the prologue in the launch the K raw planes
         const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (first ? (long long)b * a.aff_bs : (long long)b * (K + 1) * HW));
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
+        // Issue order (loads return in order): the affinities, dep and conf first — the row
+        // stores and the prologue's normalisation and conf' then run while the 2K offset planes
+        // still stream in — the offsets last (the window pass below waits for them)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(first || k < REF ? k : k + 1) * plane_bytes, ak[k]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[e] = 0.f;
+        if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
+        if (has_conf)
+            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(first ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(first || k < REF ? k : k + 1) * plane_bytes, ak[k]);
             const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
             ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dv[e] = 0.f;
-        if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
-        float cq[4] = {1.f, 1.f, 1.f, 1.f};
-        if (has_conf)
-            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(first ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
         if (first) {
             // the prologue (step 1's FIRST path, the same IEEE sequence): conf' = (1 - m) conf + m,
             // m = dep > 0 (:328-334), stored (the output dict's confidence, and the conf' other
             // parts stage from); plane 0 poisoned (iteration 1 of the launch reads it from the
             // other parts).  The affinities are normalised below, from the LDS rows.
-#pragma unroll
-            for (int e = 0; e < 4; ++e) aref[e] = 0.f;
             if (preserve) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -555,7 +560,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // stages f0 from the unrounded value, as step 1 does)
 #pragma unroll
             for (int e = 0; e < 4; ++e) cq[e] = round_to<T>(cq[e]);
-        } else {
+        }
+        if (!first) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
                 float s = 0.f;
@@ -576,7 +582,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
-            akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+            if (!first) akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
             akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
             akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
         }
@@ -617,8 +623,22 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 for (int k = 0; k < K; ++k) row[4 * k] = t1[k][0];
                 row[4 * K] = r1[0];
             }
+            // the output dict's `aff` ((K+1) planes, the normalisation's values: fp16 storage
+            // rounds them as step 1 does), streamed now, while the offsets still stream in
+            // (measured faster than one plane per iteration in the loop: C2 104.6 vs 105.8,
+            // C3 223.8 vs 227.9 us per section, profiles/r05)
+            if (active) {
+                const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + (long long)b * (K + 1) * HW);
+#pragma unroll
+                for (int c = 0; c <= K; ++c) {
+                    const float4 v = akl[c == REF ? K : (c < REF ? c : c - 1)];
+                    const float q[4] = {v.x, v.y, v.z, v.w};
+                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, q);
+                }
+            }
         }
     }
+    if (trace0 && tid == 0) trace0[4] = __builtin_amdgcn_s_memrealtime();  // (the prologue's normalisation done)
     // the quad's row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
     const auto aff4 = [&](const int k) -> float4 {
         if constexpr (TAIL) return k <= K ? aq[k < K + 1 ? k : 0] : cdl[(k - K - 1) * NT + tid];
@@ -649,12 +669,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float w_im = (float)(x0 + e - PW + jj) + hx[k][e];
                 hy[k][e] = h_im;
                 hx[k][e] = w_im;
-                if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                    hmn = fminf(hmn, h_im);
-                    hmx = fmaxf(hmx, h_im);
-                    wmn = fminf(wmn, w_im);
-                    wmx = fmaxf(wmx, w_im);
-                }
+                // branch-free: an invalid tap offers the identities (the per-tap branches and
+                // the min / max operands' canonicalisation were most of this pass)
+                const bool ok = h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf;
+                hmn = fminf(hmn, ok ? h_im : __builtin_inff());
+                hmx = fmaxf(hmx, ok ? h_im : -__builtin_inff());
+                wmn = fminf(wmn, ok ? w_im : __builtin_inff());
+                wmx = fmaxf(wmx, ok ? w_im : -__builtin_inff());
             }
         }
         if (TAIL) {  // the tail pixel's taps
@@ -700,11 +721,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int ra = max(rlo, 0), rb = min(rhi, H - 1);      // in-image window rows
     const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
     const int wqn = qb - qa + 1;
-    // (the prologue's conf' and poison stores acknowledged by every wave before the barrier
-    // behind which the part publishes: issued before the window pass, so nothing is left)
-    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
-    if (publish && tid == 0)
+    if (l2try && !first && tid == 0)  // (the prologue form publishes after its stores, below)
         __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
@@ -741,14 +759,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         has_fb = has_fb && active;
     } else {
+        const float rlof = (float)rlo, zcf = (float)(4 * wq0 - PADX);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (!(hy[k][e] > -1.f && hx[k][e] > -1.f && hy[k][e] < Hf && hx[k][e] < Wf)) {  // invalid
-                    hy[k][e] = (float)rlo;
-                    hx[k][e] = (float)(4 * wq0 - PADX);
-                }
+            for (int e = 0; e < 4; ++e) {  // (branch-free)
+                const bool ok = hy[k][e] > -1.f && hx[k][e] > -1.f && hy[k][e] < Hf && hx[k][e] < Wf;
+                hy[k][e] = ok ? hy[k][e] : rlof;  // invalid: the zero redirect
+                hx[k][e] = ok ? hx[k][e] : zcf;
             }
         }
     }
@@ -887,6 +905,13 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
         if (__builtin_amdgcn_ballot_w64(nonfin) != 0 && lane == 0) ctl[6] = 1;  // iteration 0's flag
+        // the prologue's conf' and plane-0 poison stores acknowledged by every wave, then a
+        // barrier, then the part publishes (the hand-off table's sc1 row)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (tid == 0)
+            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // Iteration t reads plane t-1 and writes plane t: t = 1 .. T-1 (the section's iterations
@@ -1061,25 +1086,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
         }
-        // the prologue's normalised affinity (the output dict's `aff`, (K+1) planes), from the
-        // quad's rows, streamed one plane per iteration: plane 0 and the reference tap's plane K/2
-        // (1 - sum as the normalisation left it) in iteration 0, plane t in iteration t, the rest
-        // in the last iteration of a short section
-        if constexpr (!TAIL) {
-            if (first && active && (t <= K || t == a.T - 1)) {
-                const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + (long long)b * (K + 1) * HW);
-                const auto put = [&](const int c) {
-                    const float4 v = akl[c == REF ? K : (c < REF ? c : c - 1)];
-                    const float q[4] = {v.x, v.y, v.z, v.w};
-                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, q);
-                };
-                if (t == 0) put(REF);
-                if (t != REF && t <= K) put(t);
-                if (t == a.T - 1)
-                    for (int c = t + 1; c <= K; ++c)
-                        if (c != REF) put(c);
-            }
-        }
         // the window holds a non-finite f (staged now, or an own quad written back after
         // the previous iteration): the reference tap takes the four-corner form below
         const bool refull = __builtin_amdgcn_readfirstlane(ctl[6 + (t & 1)]) != 0;
@@ -1118,6 +1124,32 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // later corners (gp_fail); the poison then reaches the sum as a NaN, and the abort
         // fill below the loop covers the later planes.
         bool gp_fail = false;
+        // A general-path corner's f at byte offset qo: in the prologue form's iteration 1 from
+        // the raw inputs (step 1's pass B, make_f); otherwise p_{t-1}, re-loaded until not the
+        // poison (after a step-1 launch its plane 0 never is), times conf'
+        const auto gp_corner = [&](const unsigned qo) -> float {
+            if (first && t == 0) {
+                const float p = ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.pinit) + b * HW), qo, 0u);
+                const float c = has_conf ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.conf_raw) + b * HW), qo, 0u)
+                                         : 1.f;
+                const float d = preserve ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), qo, 0u)
+                                         : 0.f;
+                return make_f<true>(p, c, d, has_conf, preserve, clip);
+            }
+            float pv = 0.f;
+            for (unsigned sp = 0;; ++sp) {  // per lane, bounded
+                bool rdy;
+                pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
+                if (rdy || (!first && t == 1) || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
+                if (sp > kResSpinLimit ||
+                    ((sp & 15u) == 15u && __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+                    gp_fail = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            return has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
+        };
         // Affinity k and 1 - sum from LDS (arow[k * astep], arow[K * astep]), or, with arow null
         // (the eight-wave build's quads: their rows are in VGPRs), re-read from global memory.
         const auto gp_pixel = [&](const int gy, const int gx, const int lcell, const unsigned gvo, const float *arow,
@@ -1166,20 +1198,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                             c4[u] = 0.f;
                             if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
                                 const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                float pv = 0.f;
-                                for (unsigned sp = 0;; ++sp) {  // per lane, bounded
-                                    bool rdy;
-                                    pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
-                                    if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
-                                    if (sp > kResSpinLimit ||
-                                        ((sp & 15u) == 15u &&
-                                         __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-                                        gp_fail = true;
-                                        break;
-                                    }
-                                    __builtin_amdgcn_s_sleep(1);
-                                }
-                                c4[u] = has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
+                                c4[u] = gp_corner(qo);
                             }
                         }
                         v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
@@ -1344,20 +1363,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                         c4[u] = 0.f;
                                         if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
                                             const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                            float pv = 0.f;
-                                            for (unsigned sp = 0;; ++sp) {  // per lane, bounded
-                                                bool rdy;
-                                                pv = ResVec<T>::template load1_p<kSc1>(rp, qo, rdy);
-                                                if (rdy || t == 1 || gp_fail || (exp_dbg(a.dbg) & 1u)) break;
-                                                if (sp > kResSpinLimit ||
-                                                    ((sp & 15u) == 15u &&
-                                                     __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-                                                    gp_fail = true;
-                                                    break;
-                                                }
-                                                __builtin_amdgcn_s_sleep(1);
-                                            }
-                                            c4[u] = has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
+                                            c4[u] = gp_corner(qo);
                                         }
                                     }
                                     v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);

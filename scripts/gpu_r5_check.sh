@@ -19,6 +19,7 @@ if [ -z "$NOBENCH" ]; then
   python -c "import json;d=json.load(open('$O/bench.json'));print('C2',d['value'],d['roofline']['kernel_ms_mean'],{k:(v['value'],v['roofline']['kernel_ms_mean']) for k,v in d['configs'].items()})"
 fi
 for CFG in ${TRACE:-nyu}; do
+  [ "$CFG" = none ] && continue
   BG=""; [ "$CFG" = kitti ] && BG="--bg 2"
   timeout -k 10 120 python tools/res_trace.py --config $CFG $BG --out $O/res_trace_$CFG.json > $O/res_trace_$CFG.log 2>&1 || { tail $O/res_trace_$CFG.log; exit 1; }
   python -c "import json;d=json.load(open('$O/res_trace_$CFG.json'));g=d['group0'];print('$CFG', {k:(v['median'] if isinstance(v,dict) and 'median' in v else v) for k,v in g.items()})"

@@ -79,6 +79,8 @@ def phases(st, it0):
     setup = {"entry_spread": su[:, 0].max() - su[:, 0].min(), "invariant_loads": np.median(su[:, 1] - su[:, 0]),
              "window": np.median(su[:, 2] - su[:, 1]), "classify": np.median(su[:, 3] - su[:, 2]),
              "geometry_to_loop": np.median(st[:, it0, 0] - su[:, 3]), "first_loop_top_max": st[:, it0, 0].max()}
+    if (su[:, 4] > 0).any():  # the prologue's normalisation done (from entry), before the loads' barrier
+        setup["normalised"] = np.median(su[:, 4] - su[:, 0])
     st = st[:, it0:, :]  # the launch's iterations (1..T with the prologue in it, else 2..T)
     ph = {"wait": st[:, :, 1] - st[:, :, 0], "stage": st[:, :, 2] - st[:, :, 1], "taps+store": st[:, :, 3] - st[:, :, 2],
           "drain+barrier": st[:, :, 4] - st[:, :, 3]}
