@@ -28,12 +28,13 @@ namespace nlspn {
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>(ResArgs);    \
     extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
 NLSPN_RES_EXTERN(float, true)
 NLSPN_RES_EXTERN(__half, true)
 NLSPN_RES_EXTERN(float, false)
 NLSPN_RES_EXTERN(__half, false)
+extern template __global__ void prop_resident_kernel<float, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
@@ -351,9 +352,12 @@ struct ResPlan {
 
 template <typename T, bool F>
 const void *res_fn_f(long long nt, bool groups) {
-    if (groups)
-        return nt == 576 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>)
-                         : reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>);
+    if (groups) {
+        if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>);
+        // (no run-time-thread-count GROUPS build of the prologue form: plan_resident never asks)
+        if constexpr (F) return nullptr;
+        else return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>);
+    }
     if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>);
     if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>);
     return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>);
@@ -482,6 +486,14 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
     // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
     if (S.nt <= 128) fp = nullptr;
+    // the run-time-thread-count GROUPS build of the prologue form holds scratch reloads in its
+    // iteration loop (tests/test_resource_usage_cpu.py): a merged multi-group launch of such a
+    // shape keeps step 1 (C3's 576-thread shape has the compile-time build)
+    {
+        const char *me = getenv("NLSPN_RES_MERGE");
+        const bool merge = B / S.Bg >= 2 && !(me && me[0] == '0');
+        if (merge && !(S.nt == 576 && pitch_ok)) fp = nullptr;
+    }
     P.first = fp != nullptr;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded); the eight-wave build keeps

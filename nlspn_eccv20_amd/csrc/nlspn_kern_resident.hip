@@ -13,13 +13,16 @@ namespace nlspn {
     template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
     template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
     template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>(ResArgs);    \
     template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
 // F: the forward prologue and iteration 1 inside the launch (ResArgs kResFirst), or after step 1
 NLSPN_RES_INST(float, true)
 NLSPN_RES_INST(__half, true)
 NLSPN_RES_INST(float, false)
 NLSPN_RES_INST(__half, false)
+// the run-time-thread-count GROUPS build: the step-1 form only (its prologue form held scratch
+// reloads in the iteration loop; the planner keeps step 1 for such merged launches)
+template __global__ void prop_resident_kernel<float, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+template __global__ void prop_resident_kernel<__half, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 // the eight-wave build (kResTailNT: affinities in VGPRs, tail pixels; fp32), launch bound 512
 // (two waves per SIMD: 256 VGPRs per lane)
 template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
