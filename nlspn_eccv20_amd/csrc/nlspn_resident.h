@@ -485,6 +485,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         unsigned x;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
         xcc_self = (x & 0xfu) + 1u;
+        // after a step-1 launch the tag only carries the placement: published at once (the
+        // prologue form publishes after its stores, below the window pass)
+        if (!first && tid == 0)
+            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
@@ -656,6 +661,23 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     if (tid == 0) { ctl[0] = 0; ctl[1] = r0; ctl[2] = r1; ctl[3] = 4 * c0; ctl[4] = 4 * c1; ctl[6] = ctl[7] = 0; }
     lds_barrier();
     if (trace0 && tid == 0) trace0[1] = __builtin_amdgcn_s_memrealtime();
+    // The output dict's inserted offsets (ResArgs::off_out: 2(K+1) planes, the reference tap's
+    // two planes zero).  The 128-thread build (small parts, C1's 247 of 72 quads: a latency-bound
+    // loop, a cheap setup) streams them from the raw offsets here, as they arrive; its loop
+    // copy cost it 13 % (216.0 k vs 197.1 k iters/s same box, profiles/r05/ab_offsetup_*.txt).
+    // The other builds (large parts: the setup is bandwidth-bound — the setup stores cost C2
+    // 8 %, C3 6 %) copy one plane per iteration in the loop (below).
+    constexpr bool OFFSETUP = NTC == 128;
+    if (OFFSETUP && a.off_out && !off_ins && active) {
+        const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
+        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < K + 1; ++c) {
+            const int k = c < REF ? c : c - 1;
+            ResVec<T>::template store<kNT>(rco, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
+            ResVec<T>::template store<kNT>(rco, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
+        }
+    }
     {
         // the extremes of the valid taps' coordinates, floored once (floor is monotonic:
         // min floor(h) = floor(min h)); a valid tap's coordinates are finite
@@ -722,9 +744,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
     const int wqn = qb - qa + 1;
     lds_barrier();
-    if (l2try && !first && tid == 0)  // (the prologue form publishes after its stores, below)
-        __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     lds_barrier();
@@ -933,7 +952,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // the reference tap's zero plane) loaded here, stored after the staging phase (by then
         // the staging waits have covered the load)
         const int cpc = t - t0;
-        const bool cpy = a.off_out != nullptr && cpc < 2 * (K + 1);
+        const bool cpy = !OFFSETUP && a.off_out != nullptr && cpc < 2 * (K + 1);
         const int cptt = cpc >> 1;
         const int cpsrc = cptt == REF ? -1 : 2 * (cptt < REF ? cptt : cptt - 1) + (cpc & 1);
         float cpq[4] = {0.f, 0.f, 0.f, 0.f}, cpq1 = 0.f;
@@ -951,7 +970,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if ((tid >> 6) == pwave) {
                 bool same = l2try, fail = false;
                 unsigned spins = 0;
-                for (int base = 0; publish && base < nparts && !fail; base += 64) {
+                // (after a step-1 launch only the placement is read: done at the first other XCC)
+                for (int base = 0; publish && base < nparts && !fail && (first || same); base += 64) {
                     const int jj = base + lane;
                     gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
                     unsigned v;
@@ -1323,20 +1343,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if constexpr (TAIL) {  // (the quad's affinities are in VGPRs: re-read from global memory)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) acc[e] = gp_pixel(y, x0 + e, lown + e, vpix + e * ES, nullptr, 0);
-                } else {  // (the same sum written out: as the lambda, the 128-thread build spilled)
+                } else {
+                    // (the same sum written out, every loop rolled: the pixel, the tap and the
+                    // corner; unrolled, this rare path's code cost the 128-thread build's loop
+                    // 3 % of C1, profiles/r05/ab_gp_r5.txt)
                     const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
-    #pragma unroll
+#pragma unroll 1
                     for (int e = 0; e < 4; ++e) {
+                        const float *arow = reinterpret_cast<const float *>(akl) + e;  // row k: arow[4 * k]
                         float s = 0.f;
-    #pragma unroll 1
+#pragma unroll 1
                         for (int k = 0; k < K; ++k) {
-                            if (k == REF) {
-                                const float4 ar = akl[K];
-                                const float arv[4] = {ar.x, ar.y, ar.z, ar.w};
-                                s += fwin[lown + e] * arv[e];
-                            }
-                            const float4 a4 = akl[k];
-                            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                            if (k == REF) s += fwin[lown + e] * arow[4 * K];
+                            const float av = arow[4 * k];
                             const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
                             const int ok = (off_ins && k >= REF) ? k + 1 : k;
                             const float h_im = (float)(y - PH + i) +
@@ -1354,24 +1373,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                                     const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
                                     v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
                                 } else {
-                                    const int h_high = h_low + 1, w_high = w_low + 1;
-                                    float c4[4];
-                                    const int cy[4] = {h_low, h_low, h_high, h_high};
-                                    const int cx[4] = {w_low, w_high, w_low, w_high};
-    #pragma unroll
+                                    // ((w1 c0 + w2 c1) + w3 c2) + w4 c3, the four-term sum's order
+#pragma unroll 1
                                     for (int u = 0; u < 4; ++u) {
-                                        c4[u] = 0.f;
-                                        if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
-                                            const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                            c4[u] = gp_corner(qo);
-                                        }
+                                        const int cy = h_low + (u >> 1), cx = w_low + (u & 1);
+                                        float c = 0.f;
+                                        if (cy >= 0 && cy <= H - 1 && cx >= 0 && cx <= W - 1)
+                                            c = gp_corner((unsigned)(cy * W + cx) * ES);
+                                        const float wu = u == 0 ? w1 : (u == 1 ? w2 : (u == 2 ? w3 : w4));
+                                        v = u == 0 ? wu * c : v + wu * c;
                                     }
-                                    v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
                                 }
                             }
-                            s += v * av[e];
+                            s += v * av;
                         }
-                        acc[e] = s;
+                        acc[0] = e == 0 ? s : acc[0];
+                        acc[1] = e == 1 ? s : acc[1];
+                        acc[2] = e == 2 ? s : acc[2];
+                        acc[3] = e == 3 ? s : acc[3];
                     }
                 }
                 gp_raise();
