@@ -950,7 +950,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         const rsrc_t rp = make_rsrc(p_all + (size_t)(t > 0 ? t - 1 : 0) * a.tstride + b * HW);
         // ---- the inserted-offset copy (ResArgs::off_out): output plane t - t0 (a raw plane, or
         // the reference tap's zero plane) loaded here, stored after the staging phase (by then
-        // the staging waits have covered the load)
+        // the staging waits have covered the load).  It costs the large builds 5 % (C2) and
+        // 9 % (C3) per section against no copy at all (timing builds, profiles/r05/
+        // ab_offcopy_cost_*.txt); stored by the setup instead it costs 8 % / 6 % more, and with
+        // its load sent straight to LDS (global_load_lds, no registers held) 1 % / 2 % more
+        // (ab_offcopy_dma_*.txt): it is traffic beside the hand-offs, not register pressure
         const int cpc = t - t0;
         const bool cpy = !OFFSETUP && a.off_out != nullptr && cpc < 2 * (K + 1);
         const int cptt = cpc >> 1;
