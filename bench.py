@@ -206,7 +206,9 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
                         "compulsory bytes of iterations 2..T over all resident launches (each plane read or "
                         "written once)" if resident else
                         "compulsory bytes per launch (each plane the launch must read or write, once)"),
-        "compulsory_bytes_per_launch": comp, "kernel_ms_mean": round(kmean, 5), "step1_kernel_ms": round(first_ms, 5),
+        "compulsory_bytes_per_launch": comp, "kernel_ms_mean": round(kmean, 5),
+        # (no step-1 launch when the resident launches run the prologue: the interval is empty)
+        "step1_kernel_ms": None if resident and first_in else round(first_ms, 5),
         "traffic_over_compulsory": round(traffic / comp, 3) if traffic else None,
         "alg_8d": {"bytes_per_launch": alg, "pixel_iterations_per_launch": npx * alg_iters,
                    "achieved": round(alg / (kmean * 1e-3) / 1e9, 1),
