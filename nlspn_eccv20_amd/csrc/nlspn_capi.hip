@@ -22,21 +22,28 @@
 #include "nlspn_s2d.h"
 #include "nlspn_heads.h"
 
-// defined in nlspn_kern_resident.hip (own translation unit and flags)
+// defined in nlspn_kern_resident.hip (3x3) and nlspn_kern_resident_wide.hip (1x17, 5x5)
+// (own translation units and flags)
 namespace nlspn {
-#define NLSPN_RES_EXTERN(T, F)                                                       \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
+#define NLSPN_RES_EXTERN(T, F)                                                                          \
+    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 0, false, F>(ResArgs);    \
+    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 576, false, F>(ResArgs);  \
+    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 128, false, F>(ResArgs);  \
+    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 576, true, F>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, F>(ResArgs);  \
+    extern template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, F>(ResArgs);
 NLSPN_RES_EXTERN(float, true)
 NLSPN_RES_EXTERN(__half, true)
 NLSPN_RES_EXTERN(float, false)
 NLSPN_RES_EXTERN(__half, false)
-extern template __global__ void prop_resident_kernel<float, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
-extern template __global__ void prop_resident_kernel<__half, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
-extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
-extern template __global__ void prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
 #define NLSPN_HD_EXTERN(MB)                                            \
     extern template __global__ void heads_kernel<MB, true>(HeadsArgs); \
@@ -350,30 +357,38 @@ struct ResPlan {
     ResArgs a[kResMaxGroups];
 };
 
-template <typename T, bool F>
+template <typename T, int KH, int KW, bool F>
 const void *res_fn_f(long long nt, bool groups) {
-    if (groups) {
-        if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, true, F>);
-        // (no run-time-thread-count GROUPS build of the prologue form: plan_resident never asks)
-        if constexpr (F) return nullptr;
-        else return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, true, F>);
+    if constexpr (KH == 5) {  // (5x5: the run-time-thread-count single-group build only)
+        if (groups) return nullptr;
+        return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 0, false, F>);
+    } else {
+        if (groups) {
+            if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 576, true, F>);
+            // (no run-time-thread-count GROUPS build of the prologue form: plan_resident never asks)
+            if constexpr (F) return nullptr;
+            else return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 0, true, F>);
+        }
+        if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 576, false, F>);
+        if constexpr (KH == 3)  // (the 128-thread build: 3x3, C1's small parts)
+            if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 128, false, F>);
+        return reinterpret_cast<const void *>(&prop_resident_kernel<T, KH, KW, kResMaxNT, kResSMax, 0, false, F>);
     }
-    if (nt == 576) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 576, false, F>);
-    if (nt == 128) return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 128, false, F>);
-    return reinterpret_cast<const void *>(&prop_resident_kernel<T, kResMaxNT, kResSMax, 0, false, F>);
 }
 
 // first: the build with the forward prologue and iteration 1 inside the launch (kResFirst)
 template <typename T>
-const void *res_fn(long long nt, bool groups, bool pitch_ok, bool tail, bool first) {
+const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first) {
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
     if (tail) {  // the eight-wave build (fp32 only; the planner checked its pitch; no prologue form)
-        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, true, false>);
-        return reinterpret_cast<const void *>(&prop_resident_kernel<float, kResTailNT, kResSMax, kResTailNT, false, false>);
+        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>);
+        return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>);
     }
-    return first ? res_fn_f<T, true>(nt, groups) : res_fn_f<T, false>(nt, groups);
+    if (kh == 1) return first ? res_fn_f<T, 1, 17, true>(nt, groups) : res_fn_f<T, 1, 17, false>(nt, groups);
+    if (kh == 5) return first ? res_fn_f<T, 5, 5, true>(nt, groups) : res_fn_f<T, 5, 5, false>(nt, groups);
+    return first ? res_fn_f<T, 3, 3, true>(nt, groups) : res_fn_f<T, 3, 3, false>(nt, groups);
 }
 
 // The part grid of a resident launch: Bg images per launch, each cut into gy row
@@ -393,8 +408,9 @@ struct ResShape {
 // in 247 parts runs 6 % faster than in 32 (same box, 222.0 k vs 209.2 k iters/s,
 // profiles/r04/ab_grid_nyu_b1_r04.txt) — round 2's cap of cus / 8 parts per image (fewer
 // neighbours to wait for under the flag hand-off) is gone.
-bool res_shape(int B, int H, int W, int cus, ResShape &S) {
-    const int W4 = W / 4;
+bool res_shape(int B, int H, int W, int kh, int kw, int cus, ResShape &S) {
+    const int W4 = W / 4, K = kh * kw - 1, px = res_px(kh, kw), tpq = 4 / px;
+    const int ry = res_ry(kh), rxq = res_rxq(kw);
     const long long Q = (long long)H * W4;
     for (int Bg = std::min(B, cus); Bg >= 1; --Bg) {
         const int gmax = (int)std::min<long long>(cus / Bg, std::max<long long>(1, Q / 64));
@@ -405,10 +421,10 @@ bool res_shape(int B, int H, int W, int cus, ResShape &S) {
                 const int gx = g / gy;
                 if (gy > H || gx > W4) continue;
                 const int ph = (H + gy - 1) / gy, pq = (W4 + gx - 1) / gx;
-                const int nq = ph * pq, nt = (nq + 63) / 64 * 64;
+                const int nq = ph * pq, nt = (nq * tpq + 63) / 64 * 64;
                 if (nt > kResMaxNT) continue;
-                const long long cells = res_win_cells(nt);
-                const long long fb = (long long)(ph + 2 * kResRY) * (4 * (pq + 2 * kResRXQ) + 2 * kResPadX);
+                const long long cells = res_win_cells(nt, res_row_bytes(K, px));
+                const long long fb = (long long)(ph + 2 * ry) * (4 * (pq + 2 * rxq) + 2 * kResPadX);
                 if (cells < fb) continue;
                 const double R = 9.0;
                 const double rim = ((ph + 2 * R) * (4.0 * pq + 2 * R) - 4.0 * nq) / 4.0;
@@ -430,7 +446,9 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                    int kw, int T, unsigned flags, ResPlan &P, void *off_out = nullptr, const ResFirst *fp = nullptr) {
     const char *env = getenv("NLSPN_RESIDENT");
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
-    if (!workspace || !off_raw || kh != 3 || kw != 3 || T < 2 || W % 4 != 0) return false;
+    if (!workspace || !off_raw || res_px(kh, kw) == 0 || T < 2 || W % 4 != 0) return false;
+    const int K = kh * kw - 1, px = res_px(kh, kw), tpq = 4 / px, ry = res_ry(kh), rxq = res_rxq(kw);
+    const int row_bytes = res_row_bytes(K, px);
     const size_t es = esize(dtype), vb = 4 * es;
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
@@ -444,17 +462,17 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const int cus = device_cus();
     if (cus < 1) return false;
     const long long HW = (long long)H * W;
-    if (HW * 9 * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into a 9-plane item
+    if (HW * 2 * (K + 1) * (long long)es > 0x7fffffffLL) return false;  // 32-bit buffer offsets into an item
     ResShape S;
-    if (!res_shape(B, H, W, cus, S)) return false;
+    if (!res_shape(B, H, W, kh, kw, cus, S)) return false;
     if (const char *gs = getenv("NLSPN_RES_GRID")) {  // A/B only: "gy,gx" or "gyxgx" part grid (same images per launch)
         int gy = 0, gx = 0;
         if (sscanf(gs, "%d%*c%d", &gy, &gx) == 2 && gy >= 1 && gx >= 1 && gy <= H && gx <= W / 4 &&
             S.Bg * gy * gx <= cus) {
-            const int ph = (H + gy - 1) / gy, pq = (W / 4 + gx - 1) / gx, nt = (ph * pq + 63) / 64 * 64;
+            const int ph = (H + gy - 1) / gy, pq = (W / 4 + gx - 1) / gx, nt = (ph * pq * tpq + 63) / 64 * 64;
             if (nt <= kResMaxNT &&
-                (long long)(ph + 2 * kResRY) * (4 * (pq + 2 * kResRXQ) + 2 * kResPadX) <= res_win_cells(nt)) {
-                S.gy = gy; S.gx = gx; S.nt = nt; S.win_cells = res_win_cells(nt);
+                (long long)(ph + 2 * ry) * (4 * (pq + 2 * rxq) + 2 * kResPadX) <= res_win_cells(nt, row_bytes)) {
+                S.gy = gy; S.gx = gx; S.nt = nt; S.win_cells = res_win_cells(nt, row_bytes);
             }
         }
     }
@@ -464,15 +482,15 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if ((size_t)(G + 1) * 4 * kResLine > kSyncBytes) return false;
     // the fixed-halo window of the largest part within the 576-thread builds' pitch / cells
     const int php = (H + S.gy - 1) / S.gy, pqp = (W / 4 + S.gx - 1) / S.gx;
-    const bool pitch_ok = 4 * (pqp + 2 * kResRXQ) + 2 * kResPadX <= res_pitch(576) &&
-                          (php + 2 * kResRY) * res_pitch(576) <= res_win_cells(576);
+    const bool pitch_ok = 4 * (pqp + 2 * rxq) + 2 * kResPadX <= res_pitch(576) &&
+                          (php + 2 * ry) * res_pitch(576) <= res_build_cells(576, 576, K, px);
     // The eight-wave build (nlspn_resident.h kResTailNT; fp32): parts of 449..576 quads
     // (C2 541.5, C3 570), whose 512 threads own a quad each and the rest as tail pixels;
     // its window has the same 128-cell pitch.  NLSPN_RES_TAIL=0 / 1 (A/B) forces the 576-thread
     // build / this one there (bit-identical); unset: kResTailDefault.
     const char *tenv = getenv("NLSPN_RES_TAIL");
     const bool tail_on = tenv && (tenv[0] == '0' || tenv[0] == '1') ? tenv[0] == '1' : kResTailDefault;
-    const bool tail = dtype == NLSPN_DTYPE_F32 && tail_on && php * pqp > kResTailNT - 64 &&
+    const bool tail = dtype == NLSPN_DTYPE_F32 && tail_on && K == 8 && php * pqp > kResTailNT - 64 &&
                       php * pqp <= kResTailNT + kResTailQuads &&
                       4 * (pqp + 2 * kResRXQ) + 2 * kResPadX <= res_pitch(kResTailNT) &&
                       (php + 2 * kResRY) * res_pitch(kResTailNT) <= kResTailWC;
@@ -491,18 +509,20 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // shape keeps step 1 (C3's 576-thread shape has the compile-time build)
     {
         const char *me = getenv("NLSPN_RES_MERGE");
-        const bool merge = B / S.Bg >= 2 && !(me && me[0] == '0');
+        // (5x5 has no GROUPS build: one launch per image group)
+        const bool merge = B / S.Bg >= 2 && !(me && me[0] == '0') && kh != 5;
         if (merge && !(S.nt == 576 && pitch_ok)) fp = nullptr;
     }
     P.first = fp != nullptr;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
     // res_win_cells, may need less: the request is padded); the eight-wave build keeps
     // conf' / dep planes and the tail pixels' planes instead of per-thread rows
-    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : 16 * kResAS * (size_t)S.nt),
+    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : (size_t)row_bytes * S.nt),
                                         80 * 1024 + 16);
     if (lds > (size_t)kResLds) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, false, pitch_ok, tail, P.first)
-                                    : res_fn<__half>(S.nt, false, pitch_ok, false, P.first);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, false, pitch_ok, tail, P.first)
+                                    : res_fn<__half>(kh, S.nt, false, pitch_ok, false, P.first);
+    if (!P.fn) return false;
     P.block = (unsigned)S.nt;
     P.lds = lds;
     P.sync_bytes = (size_t)(G + 1) * 4 * kResLine;
@@ -511,7 +531,6 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     unsigned dbg = 0;
     if (kExperiments)
         if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
-    const int K = 8;
     // Same-XCD hand-offs in the XCD's L2 (kResL2, nlspn_resident.h): possible where every
     // image plane of every iteration starts and ends on a 128-B line (no line is shared
     // by two images), not with the fused prologue; NLSPN_RES_L2=0 (A/B) keeps every
@@ -568,11 +587,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                 return false;
             }
     }
-    if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u)) {
+    if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u) && kh != 5) {
         P.a[0].ngroups = nfull;
         // the group-loop build for the merged launch; a partial last group keeps the other
-        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(S.nt, true, pitch_ok, tail, P.first)
-                                               : res_fn<__half>(S.nt, true, pitch_ok, false, P.first);
+        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, true, pitch_ok, tail, P.first)
+                                               : res_fn<__half>(kh, S.nt, true, pitch_ok, false, P.first);
         int n = 1;
         if (ng > nfull) {  // the partial group, launched after the merged one
             P.a[1] = P.a[ng - 1];

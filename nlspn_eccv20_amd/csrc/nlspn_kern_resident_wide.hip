@@ -1,0 +1,22 @@
+// Device code of the resident propagation kernel (nlspn_resident.h) for the geometries
+// beyond 3x3: 1x17 (K = 16, two pixels per thread: the C5 stress config's taps) and 5x5
+// (K = 24, a pixel per thread).  Its own translation unit, so it compiles in parallel with
+// the 3x3 builds (nlspn_kern_resident.hip); launched from nlspn_capi.hip.
+#include "nlspn_resident.h"
+
+namespace nlspn {
+// 1x17: the 576-thread builds (compile-time pitch; GROUPS for several image groups per
+// launch, the C5 shape: 16 images in 4 groups of 4) and the run-time-thread-count build
+#define NLSPN_RES_INST_W(T, F)                                                                       \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, F>(ResArgs);  \
+    template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, F>(ResArgs);
+NLSPN_RES_INST_W(float, true)
+NLSPN_RES_INST_W(__half, true)
+NLSPN_RES_INST_W(float, false)
+NLSPN_RES_INST_W(__half, false)
+// (run-time-thread-count GROUPS: the step-1 form only, as the 3x3 builds)
+template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+template __global__ void prop_resident_kernel<__half, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+}  // namespace nlspn

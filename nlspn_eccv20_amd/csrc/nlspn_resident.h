@@ -151,10 +151,22 @@ constexpr int kResPF = NLSPN_RES_PF;
 #define NLSPN_RES_WTRACE 0  // trace builds: per-wave stamps too (they cost the loop 16 B/lane of scratch)
 #endif
 constexpr bool kResWTrace = NLSPN_RES_WTRACE;
-constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo: rows, quad columns
+constexpr int kResRY = 8, kResRXQ = 2;           // fallback window halo (3x3): rows, quad columns
+// the fallback halo of a kh x kw geometry: the 3x3 one plus the taps' wider base reach
+__host__ __device__ constexpr int res_ry(int kh) { return kResRY + (kh > 3 ? (kh - 3) / 2 : 0); }
+__host__ __device__ constexpr int res_rxq(int kw) { return kResRXQ + (kw > 3 ? ((kw - 3) / 2 + 3) / 4 : 0); }
+// pixels per thread of a kh x kw geometry (a quad's 4 pixels as 1, 2 or 4 threads): the tap
+// geometry of K x PX tap-pixels lives in registers (2 per tap-pixel + half a packed index), so
+// PX shrinks as K grows — 3x3 (K = 8): 4; 1x17 (K = 16): 2; 5x5 (K = 24): 1; 0: not resident
+// (7x7, K = 48: 4 x 48 registers of tap geometry alone pass the 168-VGPR cap)
+__host__ __device__ constexpr int res_px(int kh, int kw) {
+    return (kh == 3 && kw == 3) ? 4 : (kh == 1 && kw == 17) ? 2 : (kh == 5 && kw == 5) ? 1 : 0;
+}
+// bytes of a thread's LDS rows: the K affinities, 1 - sum, conf', dep of its PX pixels
+__host__ __device__ constexpr int res_row_bytes(int K, int px) { return (K + 3) * px * 4; }
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
 constexpr int kResCtl = 8;                       // LDS control words ahead of the window
-constexpr int kResAS = 11;                       // float4 per thread: K = 8 affinities, 1 - sum, conf', dep
+constexpr int kResAS = 11;                       // float4 per thread (3x3): K = 8 affinities, 1 - sum, conf', dep
 constexpr int kResLds = 160 * 1024;              // LDS per CU
 
 // The eight-wave build (threads 512, fp32; round 5): two waves per SIMD instead of nine
@@ -173,10 +185,11 @@ __host__ __device__ constexpr int res_tail_rows_bytes() { return 16 * 2 * kResTa
 
 // LDS cells per copy of the f window for nt threads: what the per-thread rows leave,
 // a multiple of 4 (16-B aligned copies), both copies addressable by 16-bit indices.
-__host__ __device__ constexpr int res_win_cells(int nt) {
-    return ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4) < 32764
-               ? ((kResLds - 4 * kResCtl - 16 * kResAS * nt) / 8 / 4 * 4)
-               : 32764;
+// (A PITCH build's copies stay within 16-bit byte addresses: at most 8,184 cells.)
+__host__ __device__ constexpr int res_win_cells(int nt, int row_bytes = 16 * kResAS, int cap = 32764) {
+    return ((kResLds - 4 * kResCtl - row_bytes * nt) / 8 / 4 * 4) < cap
+               ? ((kResLds - 4 * kResCtl - row_bytes * nt) / 8 / 4 * 4)
+               : cap;
 }
 // The eight-wave build keeps no per-thread rows: its two copies stay within 16-bit byte
 // addresses (4 * (kResCtl + 2 * 8,184) < 65,536).
@@ -187,6 +200,10 @@ constexpr int kResTailWC = 8184;
 // 2 * 7,804 cells = 62.4 KB of byte addresses (below 64 KB: 16-bit), and for the eight-wave
 // build (2 * 8,184 cells)
 __host__ __device__ constexpr int res_pitch(int ntc) { return ntc == 576 || ntc == kResTailNT ? 128 : 0; }
+// the window cells per copy of a build (threads ntc, 0: nt at run time) and geometry
+__host__ __device__ constexpr int res_build_cells(int ntc, int nt, int K, int px) {
+    return ntc == kResTailNT ? kResTailWC : res_win_cells(ntc ? ntc : nt, res_row_bytes(K, px), res_pitch(ntc) ? 8184 : 32764);
+}
 static_assert(4 * (kResCtl + 2 * res_win_cells(576)) < 65536, "576-thread window byte addresses need 16 bits");
 static_assert(4 * (kResCtl + 2 * kResTailWC) < 65536, "eight-wave window byte addresses need 16 bits");
 
@@ -372,15 +389,99 @@ template <> struct ResVec<__half> {
     }
 };
 
+// A thread's PX pixels (PX = 4: a quad, as ResVec; 2: a pair; 1: a pixel) <-> float[PX].
+template <typename T, int PX> struct PixVec {
+    template <unsigned AUX>
+    static __device__ __forceinline__ void load(rsrc_t r, unsigned vo, unsigned so, float (&v)[PX]) {
+        if constexpr (PX == 4) {
+            ResVec<T>::template load<AUX>(r, vo, so, v);
+        } else if constexpr (PX == 1) {
+            if constexpr (sizeof(T) == 4) v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, AUX));
+            else v[0] = (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, AUX));
+        } else if constexpr (sizeof(T) == 4) {  // fp32 pair
+            const f32x2 q = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, AUX));
+            v[0] = q[0]; v[1] = q[1];
+        } else {  // fp16 pair
+            const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, AUX);
+            v[0] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu));
+            v[1] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16));
+        }
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so, const float (&v)[PX]) {
+        if constexpr (PX == 4) {
+            ResVec<T>::template store<AUX>(r, vo, so, v);
+        } else if constexpr (PX == 1) {
+            ResVec<T>::template store1<AUX>(r, vo, so, v[0]);
+        } else if constexpr (sizeof(T) == 4) {
+            const f32x2 q = {v[0], v[1]};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, q), r, vo, so, AUX);
+        } else {
+            const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, (_Float16)v[0]) |
+                               ((unsigned)__builtin_bit_cast(unsigned short, (_Float16)v[1]) << 16);
+            __builtin_amdgcn_raw_buffer_store_b32(w, r, vo, so, AUX);
+        }
+    }
+    template <unsigned AUX>
+    static __device__ __forceinline__ void poison(rsrc_t r, unsigned vo) {
+        if constexpr (PX == 4) {
+            ResVec<T>::template poison<AUX>(r, vo);
+        } else if constexpr (PX == 1) {
+            ResVec<T>::template poison1<AUX>(r, vo);
+        } else {  // (opaque: see ResVec<float>::poison)
+            unsigned p = sizeof(T) == 4 ? kResPoison32 : ((unsigned)kResPoison16 | ((unsigned)kResPoison16 << 16));
+            asm volatile("" : "+v"(p));
+            if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b64(u32x2{p, p}, r, vo, 0u, AUX);
+            else __builtin_amdgcn_raw_buffer_store_b32(p, r, vo, 0u, AUX);
+        }
+    }
+};
+// a thread's LDS row: PX floats, naturally aligned
+template <int PX> struct RowT;
+template <> struct RowT<4> { using type = float4; };
+template <> struct RowT<2> { using type = float2; };
+template <> struct RowT<1> { using type = float; };
+template <int PX> __device__ __forceinline__ void rv_get(const typename RowT<PX>::type &r, float (&v)[PX]) {
+    if constexpr (PX == 4) { v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w; }
+    else if constexpr (PX == 2) { v[0] = r.x; v[1] = r.y; }
+    else v[0] = r;
+}
+template <int PX> __device__ __forceinline__ typename RowT<PX>::type rv_make(const float (&v)[PX]) {
+    if constexpr (PX == 4) return make_float4(v[0], v[1], v[2], v[3]);
+    else if constexpr (PX == 2) return make_float2(v[0], v[1]);
+    else return v[0];
+}
+// PX cells of f into the window at cell li (li % PX == 0) and its shifted copy (fwinB[i] = f[i + 1])
+template <int PX> __device__ __forceinline__ void win_put(float *fwin, float *fwinB, int li, const float (&f)[PX]) {
+    if constexpr (PX == 4) {
+        *reinterpret_cast<float4 *>(&fwin[li]) = make_float4(f[0], f[1], f[2], f[3]);
+        fwinB[li - 1] = f[0];
+        *reinterpret_cast<float2 *>(&fwinB[li]) = make_float2(f[1], f[2]);
+        fwinB[li + 2] = f[3];
+    } else if constexpr (PX == 2) {
+        *reinterpret_cast<float2 *>(&fwin[li]) = make_float2(f[0], f[1]);
+        fwinB[li - 1] = f[0];
+        fwinB[li] = f[1];
+    } else {
+        fwin[li] = f[0];
+        fwinB[li - 1] = f[0];
+    }
+}
+
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
 // MAXNT = launch bound (threads), SMAX = staging quads per thread per round.
 // NTC = the thread count as a compile-time constant (0: blockDim.x at run time);
 // NTC = kResTailNT (512): the eight-wave build (affinities in VGPRs, tail pixels).
 // GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
 // folds away, and with it the setup spill slots it costs).
-template <typename T, int MAXNT, int SMAX, int NTC, bool GROUPS, bool FIRST>
+// KH x KW: the tap geometry; PX = res_px(KH, KW) pixels per thread (4: a quad per thread).
+template <typename T, int KH, int KW, int MAXNT, int SMAX, int NTC, bool GROUPS, bool FIRST>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
-    constexpr int KW = 3, REF = 4, K = 8, PH = 1, PW = 1, RY = kResRY, RXQ = kResRXQ, PADX = kResPadX;
+    constexpr int K = KH * KW - 1, REF = K / 2, PH = (KH - 1) / 2, PW = (KW - 1) / 2;
+    constexpr int RY = res_ry(KH), RXQ = res_rxq(KW), PADX = kResPadX;
+    constexpr int PX = res_px(KH, KW), TPQ = 4 / PX;  // pixels per thread, threads per quad
+    static_assert(PX == 1 || PX == 2 || PX == 4, "no resident form for this geometry");
+    using RowV = typename RowT<PX>::type;
     constexpr unsigned ES = sizeof(T);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // [0] abort, [1] / [2] row range, [3] / [4] column range (scratch of the setup)
@@ -390,7 +491,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // With a compile-time thread count the window size is one too (res_win_cells),
     // so every fwinB access is an immediate offset from its fwin address.
     const int NT = NTC ? NTC : (int)blockDim.x;
-    const int WC = NTC == kResTailNT ? kResTailWC : NTC ? res_win_cells(NTC) : a.win_cells;
+    const int WC = NTC ? res_build_cells(NTC, NTC, K, PX) : a.win_cells;
     // PITCH: the window's row pitch as a compile-time constant (576-thread builds: the
     // second footprint row is a ds_read immediate offset, and the window cells are kept as
     // 16-bit byte addresses, so a tap spends one VALU on its address instead of three)
@@ -398,14 +499,15 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     float *fwin = smem + kResCtl;                                            // [WH][WW] used of WC
     float *fwinB = fwin + WC;                                                // shifted by 1
-    // Per thread, kResAS float4 (thread-major, an odd count of 16-B rows: conflict-
-    // free ds_read_b128 across lanes): the K affinities, 1 - sum, the own quad's conf'
-    // (1 with conf_prop off) and dep (0 with preserve off) — every one an immediate
-    // offset from ONE address register.
-    float4 *akl = reinterpret_cast<float4 *>(fwinB + WC) + (size_t)tid * kResAS;
+    // Per thread, K + 3 rows of PX floats (thread-major, an odd count of 16-B rows at PX = 4,
+    // 8-B rows at an odd pair stride at PX = 2, odd dwords at PX = 1: conflict-free reads
+    // across lanes): the K affinities, 1 - sum, the own pixels' conf' (1 with conf_prop off)
+    // and dep (0 with preserve off) — every one an immediate offset from ONE address register.
+    RowV *akl = reinterpret_cast<RowV *>(fwinB + WC) + (size_t)tid * (K + 3);
     // the eight-wave build: the quad's affinities and 1 - sum in VGPRs (aq), its conf' / dep
     // in two float4 planes of NT (cdl), the tail pixels' values in K + 3 planes of 256 (tal)
     constexpr bool TAIL = NTC == kResTailNT;
+    static_assert(!TAIL || (K == 8 && PX == 4), "the eight-wave build is 3x3 quads");
     constexpr int SM = TAIL ? kResTailSMax : SMAX;  // staging quads per thread per round
     float4 *cdl = reinterpret_cast<float4 *>(fwinB + WC);
     float *tal = reinterpret_cast<float *>(cdl + 2 * NT) + (tid - 256);
@@ -436,7 +538,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int py = j / a.gx, px = j % a.gx;
     const int r0 = (int)((long long)py * H / a.gy), r1 = (int)((long long)(py + 1) * H / a.gy);    // own rows
     const int c0 = (int)((long long)px * W4 / a.gx), c1 = (int)((long long)(px + 1) * W4 / a.gx);  // own quad cols
-    const int nqw = c1 - c0, nown = (r1 - r0) * nqw;
+    const int nqw = c1 - c0, nownq = (r1 - r0) * nqw, nown = nownq * TPQ;  // own quads; own threads
 
     const bool has_conf = a.conf != nullptr;
     const bool preserve = (a.flags & kPreserve) != 0;
@@ -493,16 +595,16 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     }
     const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
-    if (active) {
-        const int rr = tid / nqw;
+    if (active) {  // quad tid / TPQ of the part (row-major), pixels (tid % TPQ) * PX .. + PX - 1 of it
+        const int q = TPQ == 1 ? tid : tid / TPQ, rr = q / nqw;
         y = r0 + rr;
-        x0 = 4 * (c0 + tid - rr * nqw);
+        x0 = 4 * (c0 + q - rr * nqw) + (TPQ == 1 ? 0 : (tid % TPQ) * PX);
     }
     const unsigned vpix = (unsigned)(y * W + x0) * ES;
     // ---- TAIL: pixel tj of the quads beyond the first NT (row-major in the part), one per
     // lane of waves 4..7 — one wave of each SIMD — in four contiguous chunks (consecutive
     // lanes hold consecutive pixels, so the wave's dword stores coalesce)
-    const int ntail = TAIL ? 4 * (nown - nq_main) : 0;
+    const int ntail = TAIL ? 4 * (nownq - nq_main) : 0;
     const int tchunk = (ntail + 3) >> 2;
     const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave (uniform)
     const int tj = (wvu - 4) * tchunk + lane;
@@ -515,14 +617,16 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         tx = 4 * (c0 + q - rr * nqw) + (tj & 3);
     }
     const unsigned tvpix = (unsigned)(ty * W + tx) * ES;
-    float hy[K][4], hx[K][4];
+    float hy[K][PX], hx[K][PX];
     float4 aq[K + 1];          // TAIL: the quad's affinities and 1 - sum (what akl holds otherwise)
     float thy[K] = {}, thx[K] = {};  // TAIL: the tail pixel's sample coordinates
     // the quad's affinities, dep and conf (with the prologue in the launch: raw, processed after
     // the geometry pass below, so that pass runs while they stream in)
-    float ak[K][4], dv[4], cq[4] = {1.f, 1.f, 1.f, 1.f};
+    float ak[K][PX], dv[PX], cq[PX];
+#pragma unroll
+    for (int e = 0; e < PX; ++e) cq[e] = 1.f;
     {
-        float aref[4];
+        float aref[PX];
         // the normalised (K+1)-plane layout, or with the prologue in the launch the K raw planes
         const rsrc_t ra_ = make_rsrc(static_cast<const T *>(a.aff) + (first ? (long long)b * a.aff_bs : (long long)b * (K + 1) * HW));
         const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
@@ -531,18 +635,18 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // still stream in — the offsets last (the window pass below waits for them)
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            ResVec<T>::template load<0>(ra_, vpix, (unsigned)(first || k < REF ? k : k + 1) * plane_bytes, ak[k]);
+            PixVec<T, PX>::template load<0>(ra_, vpix, (unsigned)(first || k < REF ? k : k + 1) * plane_bytes, ak[k]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dv[e] = 0.f;
-        if (preserve) ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
+        for (int e = 0; e < PX; ++e) dv[e] = 0.f;
+        if (preserve) PixVec<T, PX>::template load<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), vpix, 0u, dv);
         if (has_conf)
-            ResVec<T>::template load<0>(make_rsrc(static_cast<const T *>(first ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
+            PixVec<T, PX>::template load<0>(make_rsrc(static_cast<const T *>(first ? a.conf_raw : a.conf) + b * HW), vpix, 0u, cq);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int ok = (off_ins && k >= REF) ? k + 1 : k;  // inserted layout: skip the reference tap's planes
-            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
-            ResVec<T>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
+            PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)(2 * ok) * plane_bytes, hy[k]);
+            PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)(2 * ok + 1) * plane_bytes, hx[k]);
         }
         if (first) {
             // the prologue (step 1's FIRST path, the same IEEE sequence): conf' = (1 - m) conf + m,
@@ -551,24 +655,24 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // other parts).  The affinities are normalised below, from the LDS rows.
             if (preserve) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < PX; ++e) {
                     const float m = dv[e] > 0.f ? 1.f : 0.f;
                     cq[e] = (1.0f - m) * cq[e] + m;
                 }
             }
             if (active) {
-                if (has_conf) ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(const_cast<void *>(a.conf)) + b * HW), vpix, 0u, cq);
-                ResVec<T>::template poison<kSc1>(make_rsrc(static_cast<T *>(a.pred_inter) + b * HW), vpix);
+                if (has_conf) PixVec<T, PX>::template store<kSc1>(make_rsrc(static_cast<T *>(const_cast<void *>(a.conf)) + b * HW), vpix, 0u, cq);
+                PixVec<T, PX>::template poison<kSc1>(make_rsrc(static_cast<T *>(a.pred_inter) + b * HW), vpix);
             }
             // conf' as stored (fp16: rounded): the own quad's f_t = p_t * conf' of every later
             // iteration uses it, as the staging's loads of the stored planes do (iteration 1
             // stages f0 from the unrounded value, as step 1 does)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) cq[e] = round_to<T>(cq[e]);
+            for (int e = 0; e < PX; ++e) cq[e] = round_to<T>(cq[e]);
         }
         if (!first) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
+            for (int e = 0; e < PX; ++e) {  // reference tap weight, the step kernel's 1 - sum (same order)
                 float s = 0.f;
 #pragma unroll
                 for (int k = 0; k < K; ++k) s += ak[k][e];
@@ -578,18 +682,18 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
         // (the eight-wave build: in VGPRs, two waves per SIMD leave 256 per lane)
-        if constexpr (TAIL) {
+        if constexpr (TAIL) {  // (PX = 4)
 #pragma unroll
-            for (int k = 0; k < K; ++k) aq[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
-            aq[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-            cdl[tid] = make_float4(cq[0], cq[1], cq[2], cq[3]);
-            cdl[NT + tid] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+            for (int k = 0; k < K; ++k) aq[k] = rv_make<PX>(ak[k]);
+            aq[K] = rv_make<PX>(aref);
+            cdl[tid] = rv_make<PX>(cq);
+            cdl[NT + tid] = rv_make<PX>(dv);
         } else {
 #pragma unroll
-            for (int k = 0; k < K; ++k) akl[k] = make_float4(ak[k][0], ak[k][1], ak[k][2], ak[k][3]);
-            if (!first) akl[K] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-            akl[K + 1] = make_float4(cq[0], cq[1], cq[2], cq[3]);
-            akl[K + 2] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+            for (int k = 0; k < K; ++k) akl[k] = rv_make<PX>(ak[k]);
+            if (!first) akl[K] = rv_make<PX>(aref);
+            akl[K + 1] = rv_make<PX>(cq);
+            akl[K + 2] = rv_make<PX>(dv);
         }
         if (TAIL && wvu >= 4) {  // the tail pixel's invariants (lanes without one load pixel (r0, 4 c0): unused)
             float taf[K + 3];
@@ -618,15 +722,15 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (first) {
             const float gamma = *a.gamma;
 #pragma unroll 1
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < PX; ++e) {
                 float *row = reinterpret_cast<float *>(akl) + e;
                 float t1[K][1], r1[1];
 #pragma unroll
-                for (int k = 0; k < K; ++k) t1[k][0] = row[4 * k];
+                for (int k = 0; k < K; ++k) t1[k][0] = row[PX * k];
                 normalize_taps<K, 1>(t1, r1, a.kind, gamma);
 #pragma unroll
-                for (int k = 0; k < K; ++k) row[4 * k] = t1[k][0];
-                row[4 * K] = r1[0];
+                for (int k = 0; k < K; ++k) row[PX * k] = t1[k][0];
+                row[PX * K] = r1[0];
             }
             // the output dict's `aff` ((K+1) planes, the normalisation's values: fp16 storage
             // rounds them as step 1 does), streamed now, while the offsets still stream in
@@ -636,16 +740,16 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const rsrc_t rao = make_rsrc(static_cast<T *>(a.aff_out) + (long long)b * (K + 1) * HW);
 #pragma unroll
                 for (int c = 0; c <= K; ++c) {
-                    const float4 v = akl[c == REF ? K : (c < REF ? c : c - 1)];
-                    const float q[4] = {v.x, v.y, v.z, v.w};
-                    ResVec<T>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, q);
+                    float q[PX];
+                    rv_get<PX>(akl[c == REF ? K : (c < REF ? c : c - 1)], q);
+                    PixVec<T, PX>::template store<kNT>(rao, vpix, (unsigned)c * plane_bytes, q);
                 }
             }
         }
     }
     if (trace0 && tid == 0) trace0[4] = __builtin_amdgcn_s_memrealtime();  // (the prologue's normalisation done)
-    // the quad's row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
-    const auto aff4 = [&](const int k) -> float4 {
+    // the own pixels' row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
+    const auto aff4 = [&](const int k) -> RowV {
         if constexpr (TAIL) return k <= K ? aq[k < K + 1 ? k : 0] : cdl[(k - K - 1) * NT + tid];
         else return akl[k];
     };
@@ -670,12 +774,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr bool OFFSETUP = NTC == 128;
     if (OFFSETUP && a.off_out && !off_ins && active) {
         const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
-        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        float z[PX];
+#pragma unroll
+        for (int e = 0; e < PX; ++e) z[e] = 0.f;
 #pragma unroll
         for (int c = 0; c < K + 1; ++c) {
             const int k = c < REF ? c : c - 1;
-            ResVec<T>::template store<kNT>(rco, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
-            ResVec<T>::template store<kNT>(rco, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
+            PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)(2 * c) * plane_bytes, c == REF ? z : hy[k]);
+            PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)(2 * c + 1) * plane_bytes, c == REF ? z : hx[k]);
         }
     }
     {
@@ -686,7 +792,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         for (int k = 0; k < K; ++k) {
             const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {  // sample coordinates, .cuh:178-179
+            for (int e = 0; e < PX; ++e) {  // sample coordinates, .cuh:178-179
                 const float h_im = (float)(y - PH + i) + hy[k][e];
                 const float w_im = (float)(x0 + e - PW + jj) + hx[k][e];
                 hy[k][e] = h_im;
@@ -763,7 +869,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < PX; ++e) {
                 const float h_im = hy[k][e], w_im = hx[k][e];
                 if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
                     const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
@@ -782,7 +888,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {  // (branch-free)
+            for (int e = 0; e < PX; ++e) {  // (branch-free)
                 const bool ok = hy[k][e] > -1.f && hx[k][e] > -1.f && hy[k][e] < Hf && hx[k][e] < Wf;
                 hy[k][e] = ok ? hy[k][e] : rlof;  // invalid: the zero redirect
                 hx[k][e] = ok ? hx[k][e] : zcf;
@@ -813,16 +919,18 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // top-left corner as a float index into fwin/fwinB (the copy that makes the
     // horizontal pair 8-byte aligned), two 16-bit indices per register.  An iteration
     // then spends no VALU on floors or addresses.
-    float lhv[K][4], lwv[K][4];
-    unsigned adp[K][2];
+    float lhv[K][PX], lwv[K][PX];
+    constexpr int NSL = K * PX;  // tap-pixel slots s = k PX + e
+    unsigned adp[NSL / 2];       // slot s's footprint cell: half s & 1 of adp[s >> 1]
     {
         const float WWf = (float)WW;
         const int lbase = PADX - 4 * wq0 - rlo * WW, bofs = WC - 1;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            adp[k][0] = adp[k][1] = 0u;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < PX; ++e) {
+                const int sl = k * PX + e;
+                if ((sl & 1) == 0) adp[sl >> 1] = 0u;
                 const float fh = floorf(hy[k][e]), fw = floorf(hx[k][e]);
                 lhv[k][e] = hy[k][e] - fh;
                 lwv[k][e] = hx[k][e] - fw;
@@ -833,7 +941,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 li = ((unsigned)li < (unsigned)(WH * WW)) ? li : 0;
                 unsigned idx = (li & 1) ? (unsigned)(li + bofs) : (unsigned)li;
                 if constexpr (PITCH != 0) idx = 4u * ((unsigned)kResCtl + idx);  // byte address in the LDS
-                adp[k][e >> 1] |= idx << (16 * (e & 1));
+                adp[sl >> 1] |= idx << (16 * (sl & 1));
             }
         }
     }
@@ -865,7 +973,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int ntop = r0 - ra, nband = (ntop + rb - r1 + 1) * wqn;
     const int side = wqn - nqw, left = c0 - qa;
     // wave-uniform: held in SGPRs (as VGPRs they were the loop's one scratch reload)
-    const int nall = __builtin_amdgcn_readfirstlane((rb - ra + 1) * wqn), nrest = __builtin_amdgcn_readfirstlane(nall - nown);
+    const int nall = __builtin_amdgcn_readfirstlane((rb - ra + 1) * wqn), nrest = __builtin_amdgcn_readfirstlane(nall - nownq);
     const float rwqn = 1.0f / (float)wqn, rside = 1.0f / (float)(side > 0 ? side : 1);
 
     const T *p_all = static_cast<const T *>(a.pred_inter);
@@ -959,10 +1067,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         const bool cpy = !OFFSETUP && a.off_out != nullptr && cpc < 2 * (K + 1);
         const int cptt = cpc >> 1;
         const int cpsrc = cptt == REF ? -1 : 2 * (cptt < REF ? cptt : cptt - 1) + (cpc & 1);
-        float cpq[4] = {0.f, 0.f, 0.f, 0.f}, cpq1 = 0.f;
+        float cpq[PX], cpq1 = 0.f;
+#pragma unroll
+        for (int e = 0; e < PX; ++e) cpq[e] = 0.f;
         if (cpy && cpsrc >= 0) {
             const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
-            if (active) ResVec<T>::template load<0>(ro, vpix, (unsigned)cpsrc * plane_bytes, cpq);
+            if (active) PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)cpsrc * plane_bytes, cpq);
             if (tail_on) cpq1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)cpsrc * plane_bytes);
         }
         // ---- iteration 1, the first to read other parts' cells: wait until every part of the
@@ -1094,18 +1204,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         if (cpy) {  // streaming (nt): an output only
             const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
-            if (active) ResVec<T>::template store<kNT>(rco, vpix, (unsigned)cpc * plane_bytes, cpq);
+            if (active) PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)cpc * plane_bytes, cpq);
             if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)cpc * plane_bytes, cpq1);
             if (t == a.T - 1) {  // a short section: the planes past T - 1, here
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
                 for (int c = cpc + 1; c < 2 * (K + 1); ++c) {
                     const int tt = c >> 1, src = tt == REF ? -1 : 2 * (tt < REF ? tt : tt - 1) + (c & 1);
-                    float q[4] = {0.f, 0.f, 0.f, 0.f}, q1 = 0.f;
+                    float q[PX], q1 = 0.f;
+#pragma unroll
+                    for (int e = 0; e < PX; ++e) q[e] = 0.f;
                     if (src >= 0) {
-                        if (active) ResVec<T>::template load<0>(ro, vpix, (unsigned)src * plane_bytes, q);
+                        if (active) PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)src * plane_bytes, q);
                         if (tail_on) q1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)src * plane_bytes);
                     }
-                    if (active) ResVec<T>::template store<kNT>(rco, vpix, (unsigned)c * plane_bytes, q);
+                    if (active) PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)c * plane_bytes, q);
                     if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)c * plane_bytes, q1);
                 }
             }
@@ -1117,8 +1229,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // plane t + 1 is read by iteration t + 2 (if any): its own quad poisoned now, the
         // store acknowledged before plane t's store below (the hand-off's ordering)
         if (active && t + 2 < a.T) {
-            if (l2) ResVec<T>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
-            else ResVec<T>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
+            if (l2) PixVec<T, PX>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
+            else PixVec<T, PX>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
         }
         if (tail_on && t + 2 < a.T) {
             if (l2) ResVec<T>::template poison1<0>(make_rsrc(p_out + a.tstride), tvpix);
@@ -1132,14 +1244,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
-            asm volatile("" : "+v"(adp[k][0]), "+v"(adp[k][1]));
+            for (int e = 0; e < PX; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
+#pragma unroll
+            for (int i = k * PX / 2; i < (k + 1) * PX / 2; ++i) asm volatile("" : "+v"(adp[i]));
             if (TAIL) asm volatile("" : "+v"(tlh[k]), "+v"(tlw[k]));
         }
         if (TAIL)
 #pragma unroll
             for (int k = 0; k < K / 2; ++k) asm volatile("" : "+v"(tadp[k]));
-        float pown[4] = {0.f, 0.f, 0.f, 0.f};  // p_t of the own quad, as stored
+        float pown[PX];  // p_t of the own pixels, as stored
+#pragma unroll
+        for (int e = 0; e < PX; ++e) pown[e] = 0.f;
         // The general path's tap sum of one pixel (y, x) (window cell lcell, byte offset gvo):
         // every tap in tap order with the reference tap (weight 1 - sum, the setup's order) at
         // K/2, in the reference's per-corner form where its footprint leaves the window.
@@ -1255,9 +1370,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             tacc += v * tal[256 * k];
         };
         if (active && !(exp_dbg(a.dbg) & 4u)) {
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            float acc[PX];
+#pragma unroll
+            for (int e = 0; e < PX; ++e) acc[e] = 0.f;
             // branch-free path: every tap from the LDS window (invalid taps read zeros), in
-            // 32 tap-pixel slots s = 4k + e.  kResPF > 0 (A/B builds) issues slot s + PF's two
+            // K PX tap-pixel slots s = PX k + e (3x3 quads: 32).  kResPF > 0 (A/B builds) issues slot s + PF's two
             // footprint reads before slot s's arithmetic; the default leaves the schedule to
             // the compiler (waits per slot), which measured faster: nine waves per CU already
             // keep the LDS array busy, and its bank-conflict cycles, not the read latency,
@@ -1267,19 +1384,19 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // 576-thread builds (nine waves keep the LDS busy) lose 4 % with it
             // (profiles/r04/ab_pf_r4s_*.txt)
             // (fp32: the fp16 build spills with it)
-            constexpr int NSL = 4 * K, PF = (NTC == 128 && kResPF == 0 && ES == 4) ? 4 : kResPF;
+            constexpr int PF = (NTC == 128 && kResPF == 0 && ES == 4) ? 4 : kResPF;
             float2 g01[NSL], g23[NSL];
-            float4 akv[K + 1];
-            float4 cref;  // the reference tap's own-quad cells (one-cell form; the four-corner
-                          // form is applied after the taps, below)
+            RowV akv[K + 1];
+            RowV cref;  // the reference tap's own-pixel cells (one-cell form; the four-corner
+                        // form is applied after the taps, below)
             auto issue = [&](const int s) {
-                const int k = s >> 2, e = s & 3;
+                const int k = s / PX, e = s % PX;
                 if (e == 0) akv[k] = aff4(k);
-                if (s == 4 * REF) {  // the reference tap's own-quad cells and weight
+                if (s == PX * REF) {  // the reference tap's own-pixel cells and weight
                     akv[K] = aff4(K);
-                    cref = *reinterpret_cast<const float4 *>(&fwin[lown]);
+                    cref = *reinterpret_cast<const RowV *>(&fwin[lown]);
                 }
-                const unsigned idx = (e & 1) ? (adp[k][e >> 1] >> 16) : (adp[k][e >> 1] & 0xffffu);
+                const unsigned idx = (s & 1) ? (adp[s >> 1] >> 16) : (adp[s >> 1] & 0xffffu);
 #if NLSPN_RES_EXP == 1  // timing experiment: no gathers (wrong results)
                 g01[s] = make_float2(__builtin_bit_cast(float, idx), 1.f);
                 g23[s] = make_float2(2.f, __builtin_bit_cast(float, idx + 1u));
@@ -1309,14 +1426,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             for (int s = 0; s < NSL; ++s) {
                 if (s + PF < NSL) issue(s + PF);
                 if constexpr (PF > 0) __builtin_amdgcn_sched_barrier(0);
-                const int k = s >> 2, e = s & 3;
+                const int k = s / PX, e = s % PX;
                 if (PF == 0) issue(s);
-                if (s == 4 * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
-                    const float4 ar = akv[K];
-                    acc[0] += cref.x * ar.x; acc[1] += cref.y * ar.y; acc[2] += cref.z * ar.z; acc[3] += cref.w * ar.w;
+                if (s == PX * REF) {  // reference tap (t = K/2): zero offset, weight 1 - sum
+                    float ar[PX], cr[PX];
+                    rv_get<PX>(akv[K], ar);
+                    rv_get<PX>(cref, cr);
+#pragma unroll
+                    for (int e2 = 0; e2 < PX; ++e2) acc[e2] += cr[e2] * ar[e2];
                 }
-                const float4 a4 = akv[k];
-                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                float av[PX];
+                rv_get<PX>(akv[k], av);
                 const float lh = lhv[k][e], lw = lwv[k][e];  // = h - (float)h_low (.cuh:35-36)
                 const float hh = 1.f - lh, hw = 1.f - lw;
                 const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
@@ -1346,20 +1466,20 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const int pe = (int)(vpix / ES), y = pe / W, x0 = pe - y * W;
                 if constexpr (TAIL) {  // (the quad's affinities are in VGPRs: re-read from global memory)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[e] = gp_pixel(y, x0 + e, lown + e, vpix + e * ES, nullptr, 0);
+                    for (int e = 0; e < PX; ++e) acc[e] = gp_pixel(y, x0 + e, lown + e, vpix + e * ES, nullptr, 0);
                 } else {
                     // (the same sum written out, every loop rolled: the pixel, the tap and the
                     // corner; unrolled, this rare path's code cost the 128-thread build's loop
                     // 3 % of C1, profiles/r05/ab_gp_r5.txt)
                     const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
 #pragma unroll 1
-                    for (int e = 0; e < 4; ++e) {
-                        const float *arow = reinterpret_cast<const float *>(akl) + e;  // row k: arow[4 * k]
+                    for (int e = 0; e < PX; ++e) {
+                        const float *arow = reinterpret_cast<const float *>(akl) + e;  // row k: arow[PX * k]
                         float s = 0.f;
 #pragma unroll 1
                         for (int k = 0; k < K; ++k) {
-                            if (k == REF) s += fwin[lown + e] * arow[4 * K];
-                            const float av = arow[4 * k];
+                            if (k == REF) s += fwin[lown + e] * arow[PX * K];
+                            const float av = arow[PX * k];
                             const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
                             const int ok = (off_ins && k >= REF) ? k + 1 : k;
                             const float h_im = (float)(y - PH + i) +
@@ -1391,10 +1511,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                             }
                             s += v * av;
                         }
-                        acc[0] = e == 0 ? s : acc[0];
-                        acc[1] = e == 1 ? s : acc[1];
-                        acc[2] = e == 2 ? s : acc[2];
-                        acc[3] = e == 3 ? s : acc[3];
+#pragma unroll
+                        for (int e2 = 0; e2 < PX; ++e2) acc[e2] = e == e2 ? s : acc[e2];
                     }
                 }
                 gp_raise();
@@ -1409,15 +1527,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (refull) {
                 const float *r0p = &fwin[lown], *r1p = r0p + WW;
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < PX; ++e)
                     if (!__builtin_isfinite(r0p[e + 1]) || !__builtin_isfinite(r1p[e]) || !__builtin_isfinite(r1p[e + 1]))
                         acc[e] = __builtin_nanf("");
             }
-            float o[4], fin[4];
-            const float4 d4 = aff4(K + 2);
-            const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+            float o[PX], fin[PX], dv[PX];
+            rv_get<PX>(aff4(K + 2), dv);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < PX; ++e) {
                 float vv = acc[e];
                 if (preserve) {  // :355-357
                     const float m = dv[e] > 0.f ? 1.f : 0.f;
@@ -1429,12 +1546,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
             // plane t + 1's poison acknowledged first (issued before the taps: no wait left)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (l2) ResVec<T>::template store<0>(make_rsrc(p_out), vpix, 0u, o);  // kept in the XCD's L2
-            else ResVec<T>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
+            if (l2) PixVec<T, PX>::template store<0>(make_rsrc(p_out), vpix, 0u, o);  // kept in the XCD's L2
+            else PixVec<T, PX>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pown[e] = round_to<T>(o[e]);
+            for (int e = 0; e < PX; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
-                ResVec<T>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
+                PixVec<T, PX>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
                 }
         // ---- TAIL: the tail pixel (waves 4..7, one per SIMD), the same arithmetic in the
         // same order: taps 0..K-1 with the reference tap (one-cell form) at K/2
@@ -1479,16 +1596,15 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // ---- the own quad's f_t = p_t * conf' straight into the window, as the next
         // staging would load it
         if (t < a.T - 1 && active && !(exp_dbg(a.dbg) & 2u)) {
-            const float4 cw = aff4(K + 1);
-            float4 f = make_float4(pown[0], pown[1], pown[2], pown[3]);
-            if (has_conf) {
-                f.x = f.x * cw.x; f.y = f.y * cw.y; f.z = f.z * cw.z; f.w = f.w * cw.w;
-            }
-            *reinterpret_cast<float4 *>(&fwin[lown]) = f;
-            fwinB[lown - 1] = f.x;
-            *reinterpret_cast<float2 *>(&fwinB[lown]) = make_float2(f.y, f.z);
-            fwinB[lown + 2] = f.w;
-            if (!__builtin_isfinite((f.x + f.y) + (f.z + f.w)))
+            float cw[PX], f[PX];
+            rv_get<PX>(aff4(K + 1), cw);
+#pragma unroll
+            for (int e = 0; e < PX; ++e) f[e] = has_conf ? pown[e] * cw[e] : pown[e];
+            win_put<PX>(fwin, fwinB, lown, f);
+            float fs = f[0];
+            if constexpr (PX == 4) fs = (f[0] + f[1]) + (f[2] + f[3]);
+            else if constexpr (PX == 2) fs = f[0] + f[1];
+            if (!__builtin_isfinite(fs))
                 ctl[6 + ((t + 1) & 1)] = 1;  // (benign race: every writer stores 1)
         }
         if (tail_on && t < a.T - 1 && !(exp_dbg(a.dbg) & 2u)) {  // TAIL: the tail pixel's f_t
@@ -1502,15 +1618,22 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // read them back (rounded to fp16, the reference-tap weight 1 - sum of the rounded ones)
         if constexpr (!TAIL && ES == 2) {
             if (first && t == t0) {
-                float s4[4] = {0.f, 0.f, 0.f, 0.f};
+                float s4[PX], v[PX];
+#pragma unroll
+                for (int e = 0; e < PX; ++e) s4[e] = 0.f;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    float4 v = akl[k];
-                    v.x = round_to<T>(v.x); v.y = round_to<T>(v.y); v.z = round_to<T>(v.z); v.w = round_to<T>(v.w);
-                    akl[k] = v;
-                    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
+                    rv_get<PX>(akl[k], v);
+#pragma unroll
+                    for (int e = 0; e < PX; ++e) {
+                        v[e] = round_to<T>(v[e]);
+                        s4[e] += v[e];
+                    }
+                    akl[k] = rv_make<PX>(v);
                 }
-                akl[K] = make_float4(1.0f - s4[0], 1.0f - s4[1], 1.0f - s4[2], 1.0f - s4[3]);
+#pragma unroll
+                for (int e = 0; e < PX; ++e) s4[e] = 1.0f - s4[e];
+                akl[K] = rv_make<PX>(s4);
             }
         }
     }
@@ -1520,12 +1643,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // the loop scratch.)
     if (t_abort) {
         if (active) {
-            const float qn[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+            float qn[PX];
+#pragma unroll
+            for (int e = 0; e < PX; ++e) qn[e] = __builtin_nanf("");
             for (int g2 = grp; g2 < ngroups; ++g2) {
                 const int b2 = bl + g2 * a.B;
                 for (int tt = g2 == grp ? t_abort : t0; tt < a.T; ++tt)
-                    ResVec<T>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
-                ResVec<T>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
+                    PixVec<T, PX>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
+                PixVec<T, PX>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
             }
         }
         if (tail_on) {

@@ -27,9 +27,9 @@ def cu(x, dtype=torch.float32):
     return None if x is None else torch.from_numpy(np.ascontiguousarray(x)).to(DEV, dtype)
 
 
-def resident_config(B, H, W, dtype=0, conf=True, T=18):
+def resident_config(B, H, W, dtype=0, conf=True, T=18, kernel=(3, 3)):
     g, b, l = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    ok = _lib.get().nlspn_resident_config(dtype, B, H, W, 3, 3, T, int(conf), ctypes.byref(g), ctypes.byref(b),
+    ok = _lib.get().nlspn_resident_config(dtype, B, H, W, kernel[0], kernel[1], T, int(conf), ctypes.byref(g), ctypes.byref(b),
                                           ctypes.byref(l))
     return bool(ok), g.value, b.value, l.value
 
@@ -49,11 +49,11 @@ class _env:
             os.environ[self.name] = self.old
 
 
-def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=0.05):
-    s = synth(B, H, W, 8, seed=seed, off_sigma=sigma, density=density)
+def _inputs(B, H, W, sigma=2.0, seed=3, dtype=torch.float32, conf=True, density=0.05, K=8):
+    s = synth(B, H, W, K, seed=seed, off_sigma=sigma, density=density)
     oa = cu(s["off_aff"], dtype)
     return (cu(s["pred_init"], dtype), cu(s["dep"], dtype), cu(s["conf"], dtype) if conf else None,
-            oa[:, 16:], oa[:, :16], torch.tensor([4.0], device=DEV)), s
+            oa[:, 2 * K:], oa[:, :2 * K], torch.tensor([4.0], device=DEV)), s
 
 
 def _nan_equal(x, y):
@@ -155,6 +155,28 @@ def test_resident_bitexact_vs_steps(B, H, W, sigma, dtype, conf, kw):
         assert resident_config(B, H, W, 0 if dtype == torch.float32 else 1, conf)[0]
     inp, _ = _inputs(B, H, W, sigma=sigma, dtype=dtype, conf=conf)
     a, b = _both(inp, **kw)
+    assert torch.equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
+    assert torch.equal(a["pred"], b["pred"])
+
+
+@pytest.mark.parametrize("B,H,W,sigma,dtype,kernel,T", [
+    (16, 228, 304, 2.0, torch.float16, (1, 17), 36),   # C5: four image groups of four, one launch
+    (16, 228, 304, 2.0, torch.float32, (1, 17), 36),   # C5 shape, fp32 storage
+    (4, 96, 128, 3.0, torch.float32, (1, 17), 18),
+    (3, 64, 96, 12.0, torch.float16, (1, 17), 18),     # taps beyond the halo (general path)
+    (1, 24, 32, 2.0, torch.float16, (1, 17), 5),       # tiny parts
+    (2, 64, 96, 2.0, torch.float32, (5, 5), 18),
+    (2, 60, 128, 6.0, torch.float16, (5, 5), 18),
+    (8, 228, 304, 2.0, torch.float16, (5, 5), 6),      # one launch per image group (no GROUPS build)
+])
+def test_resident_wide_geometry_bitexact(B, H, W, sigma, dtype, kernel, T):
+    """The resident kernel's 1x17 (two pixels per thread) and 5x5 (a pixel per thread)
+    builds: bit-exact against the step launches, every plane, both resident forms."""
+    K = kernel[0] * kernel[1] - 1
+    with _env("1"):
+        assert resident_config(B, H, W, 0 if dtype == torch.float32 else 1, True, T, kernel)[0]
+    inp, _ = _inputs(B, H, W, sigma=sigma, dtype=dtype, K=K)
+    a, b = _both(inp, T=T, kernel=kernel)
     assert torch.equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
     assert torch.equal(a["pred"], b["pred"])
 

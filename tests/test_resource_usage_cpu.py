@@ -35,7 +35,7 @@ RESIDENT_LOOP_RELOADS_F16 = 0     # the fp16 builds alike
 
 
 def _groups(name):
-    # template <T, MAXNT, SMAX, NTC, GROUPS, FIRST>: GROUPS is the first of the two bools
+    # template <T, KH, KW, MAXNT, SMAX, NTC, GROUPS, FIRST>: GROUPS is the first of the two bools
     return re.search(r"ELb1ELb[01]EEEv", name) is not None
 
 
@@ -81,11 +81,13 @@ def test_resident_kernel_registers_and_scratch():
     assert any(_groups(n) for n in res) and any(not _groups(n) for n in res), "GROUPS builds missing"
     assert all(r.get("ScratchSize", 0) <= (RESIDENT_SCRATCH_CAP_GROUPS if _groups(n) else RESIDENT_SCRATCH_CAP)
                for n, r in res.items()), res
-    out = subprocess.run(["/opt/rocm/bin/hipcc", *_FLAGS, "--cuda-device-only", "-S", "-o", "/tmp/nlspn_res_test.s",
-                          os.path.join(CSRC, "nlspn_kern_resident.hip")], capture_output=True, text=True, cwd=CSRC)
-    assert out.returncode == 0, out.stderr[-2000:]
-    with open("/tmp/nlspn_res_test.s") as f:
-        asm = f.read()
+    asm = ""
+    for tu in ("nlspn_kern_resident.hip", "nlspn_kern_resident_wide.hip"):  # 3x3; 1x17 and 5x5
+        out = subprocess.run(["/opt/rocm/bin/hipcc", *_FLAGS, "--cuda-device-only", "-S", "-o", "/tmp/nlspn_res_test.s",
+                              os.path.join(CSRC, tu)], capture_output=True, text=True, cwd=CSRC)
+        assert out.returncode == 0, out.stderr[-2000:]
+        with open("/tmp/nlspn_res_test.s") as f:
+            asm += f.read()
     for name in res:
         loop = RU.loop_scratch(asm, name, 2 if _groups(name) else 1)["loop"]
         cap = RESIDENT_LOOP_RELOADS_F16 if "6__half" in name else RESIDENT_LOOP_RELOADS
