@@ -29,15 +29,19 @@ namespace nlspn {
     extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 0, false, F>(ResArgs);    \
     extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 576, false, F>(ResArgs);  \
     extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 128, false, F>(ResArgs);  \
-    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 576, true, F>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
-    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
-    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, F>(ResArgs);  \
-    extern template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, F>(ResArgs);
+    extern template __global__ void prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 576, true, F>(ResArgs);
 NLSPN_RES_EXTERN(float, true)
 NLSPN_RES_EXTERN(__half, true)
 NLSPN_RES_EXTERN(float, false)
 NLSPN_RES_EXTERN(__half, false)
+// (the wider geometries: the step-1 form only, plan_resident)
+#define NLSPN_RES_EXTERN_W(T)                                                                              \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, false>(ResArgs);   \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, false>(ResArgs); \
+    extern template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, false>(ResArgs);  \
+    extern template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, false>(ResArgs);
+NLSPN_RES_EXTERN_W(float)
+NLSPN_RES_EXTERN_W(__half)
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
@@ -386,8 +390,9 @@ const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, 
         if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>);
         return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>);
     }
-    if (kh == 1) return first ? res_fn_f<T, 1, 17, true>(nt, groups) : res_fn_f<T, 1, 17, false>(nt, groups);
-    if (kh == 5) return first ? res_fn_f<T, 5, 5, true>(nt, groups) : res_fn_f<T, 5, 5, false>(nt, groups);
+    // (the wider geometries: the step-1 form only, plan_resident)
+    if (kh == 1) return first ? nullptr : res_fn_f<T, 1, 17, false>(nt, groups);
+    if (kh == 5) return first ? nullptr : res_fn_f<T, 5, 5, false>(nt, groups);
     return first ? res_fn_f<T, 3, 3, true>(nt, groups) : res_fn_f<T, 3, 3, false>(nt, groups);
 }
 
@@ -412,7 +417,9 @@ bool res_shape(int B, int H, int W, int kh, int kw, int cus, ResShape &S) {
     const int W4 = W / 4, K = kh * kw - 1, px = res_px(kh, kw), tpq = 4 / px;
     const int ry = res_ry(kh), rxq = res_rxq(kw);
     const long long Q = (long long)H * W4;
-    for (int Bg = std::min(B, cus); Bg >= 1; --Bg) {
+    // the rim's reach: ~9 px for 3x3, plus the wider geometries' tap reach (1x17: 8 x 16)
+    const double Ry = 9.0 + (kh - 3) / 2, Rx = 9.0 + (kw - 3) / 2;
+    const auto search = [&](int Bg) {  // the best part grid for Bg images per launch
         const int gmax = (int)std::min<long long>(cus / Bg, std::max<long long>(1, Q / 64));
         double best = 1e300;
         for (int g = gmax; g >= std::max(1, gmax * 3 / 4); --g) {
@@ -426,8 +433,7 @@ bool res_shape(int B, int H, int W, int kh, int kw, int cus, ResShape &S) {
                 const long long cells = res_win_cells(nt, res_row_bytes(K, px));
                 const long long fb = (long long)(ph + 2 * ry) * (4 * (pq + 2 * rxq) + 2 * kResPadX);
                 if (cells < fb) continue;
-                const double R = 9.0;
-                const double rim = ((ph + 2 * R) * (4.0 * pq + 2 * R) - 4.0 * nq) / 4.0;
+                const double rim = ((ph + 2 * Ry) * (4.0 * pq + 2 * Rx) - 4.0 * nq) / 4.0;
                 const double cost = nq + 0.2 * rim;
                 if (cost < best) {
                     best = cost;
@@ -435,7 +441,15 @@ bool res_shape(int B, int H, int W, int kh, int kw, int cus, ResShape &S) {
                 }
             }
         }
-        if (best < 1e300) return true;
+        return best < 1e300;
+    };
+    for (int Bg = std::min(B, cus); Bg >= 1; --Bg) {
+        if (!search(Bg)) continue;
+        // the same number of launches with the images spread evenly: smaller parts (C5, 16
+        // images: 4 groups of 4 in parts of 286 quads, not 3 of 5 and 1 of 1 in parts of 363)
+        const int ng = (B + Bg - 1) / Bg, Be = (B + ng - 1) / ng;
+        if (Be < Bg) search(Be);  // (feasible: more parts per image, each smaller)
+        return true;
     }
     return false;
 }
@@ -504,6 +518,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
     // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
     if (S.nt <= 128) fp = nullptr;
+    // The wider geometries (two or one pixel per thread) load their raw planes in 4-B (fp16
+    // pairs) or smaller pieces: the prologue's loads from HBM take C5's setup 14.2 us per
+    // image group where step 1's L2-hot outputs take 4.8 (traces), 690 vs 662 us per section
+    // same-process (profiles/r05/ab_first_c5_r5.json): step 1 stays in front of them
+    if (px < 4) fp = nullptr;
     // the run-time-thread-count GROUPS build of the prologue form holds scratch reloads in its
     // iteration loop (tests/test_resource_usage_cpu.py): a merged multi-group launch of such a
     // shape keeps step 1 (C3's 576-thread shape has the compile-time build)

@@ -6,17 +6,15 @@
 
 namespace nlspn {
 // 1x17: the 576-thread builds (compile-time pitch; GROUPS for several image groups per
-// launch, the C5 shape: 16 images in 4 groups of 4) and the run-time-thread-count build
-#define NLSPN_RES_INST_W(T, F)                                                                       \
-    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, F>(ResArgs);   \
-    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, F>(ResArgs); \
-    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, F>(ResArgs);  \
-    template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, F>(ResArgs);
-NLSPN_RES_INST_W(float, true)
-NLSPN_RES_INST_W(__half, true)
-NLSPN_RES_INST_W(float, false)
-NLSPN_RES_INST_W(__half, false)
-// (run-time-thread-count GROUPS: the step-1 form only, as the 3x3 builds)
-template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
-template __global__ void prop_resident_kernel<__half, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+// launch, the C5 shape: 16 images in 4 groups of 4) and the run-time-thread-count builds.
+// The step-1 form only (FIRST = false): a thread's raw-plane loads are 4 B or less, and the
+// prologue's loads from HBM cost C5 more than step 1 does (nlspn_capi.hip plan_resident).
+#define NLSPN_RES_INST_W(T)                                                                            \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, false, false>(ResArgs);   \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, false, false>(ResArgs); \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 576, true, false>(ResArgs);  \
+    template __global__ void prop_resident_kernel<T, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);    \
+    template __global__ void prop_resident_kernel<T, 5, 5, kResMaxNT, kResSMax, 0, false, false>(ResArgs);
+NLSPN_RES_INST_W(float)
+NLSPN_RES_INST_W(__half)
 }  // namespace nlspn

@@ -132,6 +132,10 @@ def test_resident_engaged_at_c2():
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
         ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in 13 x 19 parts of 72 quads
         assert ok and grid == 247 and block == 128
+        # C5 (1x17, fp16, 16 images): four groups of four images in 9 x 7 parts of 286 quads, two
+        # threads per quad (the 576-thread build; not three groups of five and one of one)
+        ok, grid, block, lds = resident_config(16, 228, 304, dtype=1, T=36, kernel=(1, 17))
+        assert ok and grid == 4 * 63 and block == 576
 
 
 @pytest.mark.parametrize("B,H,W,sigma,dtype,conf,kw", [

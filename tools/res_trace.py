@@ -4,7 +4,7 @@ staging (S1), after the staging barrier (S2: staging includes the spin on poison
 i.e. the hand-off latency plus the skew to the slowest producer), taps + stores issued
 (S3), after the closing barrier (S4) — into the `pred` buffer.  Prints per-phase medians
 (us) per image-group launch.  Builds with NLSPN_RES_WTRACE=1 add per-wave stamps.
-usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1] [--bg IMAGES_PER_LAUNCH] [--out FILE]"""
+usage: python tools/res_trace.py [--config nyu|kitti|nyu_b1|nyu_k16] [--bg IMAGES_PER_LAUNCH] [--out FILE]"""
 import ctypes
 import json
 import os
@@ -22,36 +22,43 @@ from nlspn_eccv20_amd.propagation import _alloc_outputs, _propagate_args, _strea
 from nlspn_eccv20_amd.synthetic import synth  # noqa: E402
 
 
-CONFIGS = {"nyu": (8, 228, 304, 500 / (228 * 304)), "kitti": (4, 240, 1216, 0.05), "nyu_b1": (1, 228, 304, 500 / (228 * 304))}
+# B, H, W, density, tap geometry, T, storage
+_NYU = 500 / (228 * 304)
+CONFIGS = {"nyu": (8, 228, 304, _NYU, (3, 3), 18, torch.float32), "kitti": (4, 240, 1216, 0.05, (3, 3), 18, torch.float32),
+           "nyu_b1": (1, 228, 304, _NYU, (3, 3), 18, torch.float32),
+           "nyu_k16": (16, 228, 304, _NYU, (1, 17), 36, torch.float16)}
 
 
-def main(config="nyu", T=18, reps=5, bg=None, out=None):
-    B, H, W, density = CONFIGS[config]
+def main(config="nyu", reps=5, bg=None, out=None):
+    B, H, W, density, kern, T, dt = CONFIGS[config]
+    K = kern[0] * kern[1] - 1
     dev = torch.device("cuda", 0)
-    s = synth(B, H, W, 8, seed=7240, off_sigma=2.0, density=density)
-    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+    s = synth(B, H, W, K, seed=7240, off_sigma=2.0, density=density)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev, dt)  # noqa: E731
     oa = t(s["off_aff"])
-    ins = (t(s["pred_init"]), t(s["dep"]), t(s["conf"]), oa[:, 16:], oa[:, :16], torch.tensor([4.0], device=dev))
+    ins = (t(s["pred_init"]), t(s["dep"]), t(s["conf"]), oa[:, 2 * K:], oa[:, :2 * K], torch.tensor([4.0], device=dev))
     lib = _lib.get()
-    grid = ctypes.c_int()
+    grid, blk = ctypes.c_int(), ctypes.c_int()
     os.environ["NLSPN_RESIDENT"] = "1"
-    lib.nlspn_resident_config(0, B, H, W, 3, 3, T, 1, ctypes.byref(grid), None, None)
+    lib.nlspn_resident_config(0 if dt == torch.float32 else 1, B, H, W, kern[0], kern[1], T, 1, ctypes.byref(grid),
+                              ctypes.byref(blk), None)
     G = grid.value  # parts of one image-group launch
     bg = bg or B    # images per launch (C3: 2)
     ng = (B + bg - 1) // bg
     g = G // bg
     os.environ["NLSPN_RES_DBG"] = "8"
-    outs = _alloc_outputs(ins[0], 8, T, True, True)
-    args, _ = _propagate_args(*ins, (3, 3), T, "TGASS", True, False, outs)
+    outs = _alloc_outputs(ins[0], K, T, True, True)
+    args, _ = _propagate_args(*ins, kern, T, "TGASS", True, False, outs)
     for _ in range(reps):
         _lib.check(lib.nlspn_propagate(*args, _stream(dev)))
     torch.cuda.synchronize()
     os.environ.pop("NLSPN_RES_DBG")
     HW = H * W
     allst = outs["pred"].view(-1).view(torch.int64).cpu().numpy()
+    ept = 8 // outs["pred"].element_size()  # pred elements per int64 stamp
     res = {}
     for grp in range(ng):
-        o = grp * bg * HW // 2  # group k's stamps start at its own pred planes (int64 = 2 floats)
+        o = grp * bg * HW // ept  # group k's stamps start at its own pred planes
         R = T + 1  # rows per part: the setup, then iteration t in row t + 1
         raw = allst[o: o + G * R * 5].reshape(G, R, 5)
         # with the prologue in the launch iteration 0 (the section's iteration 1) has a row;
@@ -66,7 +73,8 @@ def main(config="nyu", T=18, reps=5, bg=None, out=None):
             s2 = raw[:, :, 2]
             if (wv[:, 0, :, 0] != 0).any():  # builds with per-wave stamps (NLSPN_RES_WTRACE=1)
                 res[f"group{grp}"]["waves"] = waves(s2, wv, it0)
-    line = json.dumps({"config": config, "parts_per_launch": G, "images_per_launch": bg, "groups": ng, **res})
+    line = json.dumps({"config": config, "parts_per_launch": G, "threads": blk.value, "images_per_launch": bg,
+                       "groups": ng, **res})
     if out:  # the JSON alone (the runtime's stderr lines never land in the file)
         with open(out, "w") as f:
             f.write(line + "\n")
