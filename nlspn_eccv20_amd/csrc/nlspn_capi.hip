@@ -46,6 +46,8 @@ extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kRe
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<__half, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
@@ -382,7 +384,9 @@ const void *res_fn_f(long long nt, bool groups) {
 
 // first: the build with the forward prologue and iteration 1 inside the launch (kResFirst)
 template <typename T>
-const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first) {
+const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first, bool split = false) {
+    // the split-quad build (3x3, two threads per quad, 192 threads, one image group, step-1 form)
+    if (split) return groups || first ? nullptr : reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>);
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
@@ -462,7 +466,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     if (env && env[0] == '0') return false;  // A/B: force the per-iteration launches
     if (!workspace || !off_raw || res_px(kh, kw) == 0 || T < 2 || W % 4 != 0) return false;
     const int K = kh * kw - 1, px = res_px(kh, kw), tpq = 4 / px, ry = res_ry(kh), rxq = res_rxq(kw);
-    const int row_bytes = res_row_bytes(K, px);
+    int row_bytes = res_row_bytes(K, px);
     const size_t es = esize(dtype), vb = 4 * es;
     if (!aligned(conf_eff, vb) || !aligned(dep, vb) || !aligned(aff_norm, vb) || !aligned(off_raw, vb) ||
         !aligned(pred_inter, vb) || !aligned(pred, vb) || off_bs % 4 != 0 || !aligned(workspace, 16))
@@ -518,6 +522,24 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
     // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
     if (S.nt <= 128) fp = nullptr;
+    // Split quads: 3x3 parts of at most two waves in one image group (C1: 247 parts of 72
+    // quads) run two threads per quad (192 threads), halving each thread's latency-bound chain
+    // of tap-pixel slots; NLSPN_RES_SPLIT=0 (A/B) keeps a thread per quad
+    bool split = false;
+    if (kh == 3 && S.nt <= 128 && !tail && B <= S.Bg) {
+        const char *se = getenv("NLSPN_RES_SPLIT");
+        const int nt2 = (php * pqp * 2 + 63) / 64 * 64;
+        const int rb2 = res_row_bytes(K, 2);
+        const int cells2 = res_win_cells(192, rb2);
+        if (!(se && se[0] == '0') && nt2 == 192 &&
+            (long long)(php + 2 * ry) * (4 * (pqp + 2 * rxq) + 2 * kResPadX) <= cells2) {
+            split = true;
+            S.nt = 192;
+            S.win_cells = cells2;
+            row_bytes = rb2;
+            fp = nullptr;
+        }
+    }
     // The wider geometries (two or one pixel per thread) load their raw planes in 4-B (fp16
     // pairs) or smaller pieces: the prologue's loads from HBM take C5's setup 14.2 us per
     // image group where step 1's L2-hot outputs take 4.8 (traces), 690 vs 662 us per section
@@ -539,8 +561,8 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : (size_t)row_bytes * S.nt),
                                         80 * 1024 + 16);
     if (lds > (size_t)kResLds) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, false, pitch_ok, tail, P.first)
-                                    : res_fn<__half>(kh, S.nt, false, pitch_ok, false, P.first);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, false, pitch_ok, tail, P.first, split)
+                                    : res_fn<__half>(kh, S.nt, false, pitch_ok, false, P.first, split);
     if (!P.fn) return false;
     P.block = (unsigned)S.nt;
     P.lds = lds;

@@ -475,11 +475,15 @@ template <int PX> __device__ __forceinline__ void win_put(float *fwin, float *fw
 // GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
 // folds away, and with it the setup spill slots it costs).
 // KH x KW: the tap geometry; PX = res_px(KH, KW) pixels per thread (4: a quad per thread).
-template <typename T, int KH, int KW, int MAXNT, int SMAX, int NTC, bool GROUPS, bool FIRST>
+// PXO: pixels per thread overriding res_px (0: res_px): small latency-bound parts (a B = 1 NYU
+// image in 247 parts of 72 quads) split a 3x3 quad over two threads, halving each thread's
+// dependency chain of tap-pixel slots.
+template <typename T, int KH, int KW, int MAXNT, int SMAX, int NTC, bool GROUPS, bool FIRST, int PXO = 0>
 __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int K = KH * KW - 1, REF = K / 2, PH = (KH - 1) / 2, PW = (KW - 1) / 2;
     constexpr int RY = res_ry(KH), RXQ = res_rxq(KW), PADX = kResPadX;
-    constexpr int PX = res_px(KH, KW), TPQ = 4 / PX;  // pixels per thread, threads per quad
+    constexpr int PX = PXO ? PXO : res_px(KH, KW), TPQ = 4 / PX;  // pixels per thread, threads per quad
+    static_assert(!(PXO && FIRST), "the split-quad builds run behind step 1");
     static_assert(PX == 1 || PX == 2 || PX == 4, "no resident form for this geometry");
     using RowV = typename RowT<PX>::type;
     constexpr unsigned ES = sizeof(T);
@@ -771,7 +775,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // copy cost it 13 % (216.0 k vs 197.1 k iters/s same box, profiles/r05/ab_offsetup_*.txt).
     // The other builds (large parts: the setup is bandwidth-bound — the setup stores cost C2
     // 8 %, C3 6 %) copy one plane per iteration in the loop (below).
-    constexpr bool OFFSETUP = NTC == 128;
+    constexpr bool OFFSETUP = NTC == 128 || PXO != 0;
     if (OFFSETUP && a.off_out && !off_ins && active) {
         const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
         float z[PX];
@@ -1384,7 +1388,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             // 576-thread builds (nine waves keep the LDS busy) lose 4 % with it
             // (profiles/r04/ab_pf_r4s_*.txt)
             // (fp32: the fp16 build spills with it)
-            constexpr int PF = (NTC == 128 && kResPF == 0 && ES == 4) ? 4 : kResPF;
+            constexpr int PF = ((NTC == 128 || PXO != 0) && kResPF == 0 && ES == 4) ? 4 : kResPF;
             float2 g01[NSL], g23[NSL];
             RowV akv[K + 1];
             RowV cref;  // the reference tap's own-pixel cells (one-cell form; the four-corner
