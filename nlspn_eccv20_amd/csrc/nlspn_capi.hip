@@ -48,6 +48,8 @@ extern template __global__ void prop_resident_kernel<float, 1, 17, kResMaxNT, kR
 extern template __global__ void prop_resident_kernel<__half, 1, 17, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
@@ -384,9 +386,13 @@ const void *res_fn_f(long long nt, bool groups) {
 
 // first: the build with the forward prologue and iteration 1 inside the launch (kResFirst)
 template <typename T>
-const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first, bool split = false) {
-    // the split-quad build (3x3, two threads per quad, 192 threads, one image group, step-1 form)
-    if (split) return groups || first ? nullptr : reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>);
+const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first, int split = 0) {
+    // the split-quad builds (3x3, `split` pixels per thread: 2 at 192 threads, 1 at 320; one
+    // image group, step-1 form)
+    if (split)
+        return groups || first ? nullptr
+               : split == 1 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>)
+                            : reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>);
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
@@ -523,21 +529,23 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
     if (S.nt <= 128) fp = nullptr;
     // Split quads: 3x3 parts of at most two waves in one image group (C1: 247 parts of 72
-    // quads) run two threads per quad (192 threads), halving each thread's latency-bound chain
-    // of tap-pixel slots; NLSPN_RES_SPLIT=0 (A/B) keeps a thread per quad
-    bool split = false;
+    // quads) run four threads per quad (320 threads) or two (192), cutting each thread's
+    // latency-bound chain of tap-pixel slots from 32 to 8 or 16; NLSPN_RES_SPLIT=0 / 2 (A/B)
+    // keeps a thread per quad / forces two
+    int split = 0;
     if (kh == 3 && S.nt <= 128 && !tail && B <= S.Bg) {
         const char *se = getenv("NLSPN_RES_SPLIT");
-        const int nt2 = (php * pqp * 2 + 63) / 64 * 64;
-        const int rb2 = res_row_bytes(K, 2);
-        const int cells2 = res_win_cells(192, rb2);
-        if (!(se && se[0] == '0') && nt2 == 192 &&
-            (long long)(php + 2 * ry) * (4 * (pqp + 2 * rxq) + 2 * kResPadX) <= cells2) {
-            split = true;
-            S.nt = 192;
-            S.win_cells = cells2;
-            row_bytes = rb2;
-            fp = nullptr;
+        const int want = se && (se[0] == '0' || se[0] == '2') ? se[0] - '0' : 1;
+        for (int sp = want; sp >= 1 && sp <= 2 && !split; ++sp) {
+            const int ntc = sp == 1 ? 320 : 192, nts = (php * pqp * (4 / sp) + 63) / 64 * 64;
+            const int rbs = res_row_bytes(K, sp), cells = res_win_cells(ntc, rbs);
+            if (nts <= ntc && (long long)(php + 2 * ry) * (4 * (pqp + 2 * rxq) + 2 * kResPadX) <= cells) {
+                split = sp;
+                S.nt = ntc;
+                S.win_cells = cells;
+                row_bytes = rbs;
+                fp = nullptr;
+            }
         }
     }
     // The wider geometries (two or one pixel per thread) load their raw planes in 4-B (fp16

@@ -25,9 +25,12 @@ NLSPN_RES_INST(__half, false)
 // reloads in the iteration loop; the planner keeps step 1 for such merged launches)
 template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
 template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 0, true, false>(ResArgs);
-// the split-quad build (two threads per quad, 192 threads: small 3x3 parts, C1; step-1 form)
+// the split-quad builds (small 3x3 parts, C1; step-1 form): four threads per quad at 320
+// threads, two at 192
 template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
 template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
+template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
+template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
 // the eight-wave build (kResTailNT: affinities in VGPRs, tail pixels; fp32), launch bound 512
 // (two waves per SIMD: 256 VGPRs per lane)
 template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);

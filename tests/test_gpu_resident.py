@@ -80,8 +80,10 @@ def _both(inp, T=18, nan_ok=False, **kw):
             d = propagate(*inp, prop_time=T, **kw)
         with _env("0", "NLSPN_RES_FIRST"):
             f = propagate(*inp, prop_time=T, **kw)
-        with _env("0", "NLSPN_RES_SPLIT"):  # (small parts: one thread per quad instead of two)
+        with _env("0", "NLSPN_RES_SPLIT"):  # (small parts: one thread per quad instead of four)
             g = propagate(*inp, prop_time=T, **kw)
+        with _env("2", "NLSPN_RES_SPLIT"):  # (two threads per quad)
+            h = propagate(*inp, prop_time=T, **kw)
     with _env("0"):
         b = propagate(*inp, prop_time=T, **kw)
     torch.cuda.synchronize()
@@ -100,6 +102,8 @@ def _both(inp, T=18, nan_ok=False, **kw):
     assert eq(a["pred"], f["pred"])
     assert eq(a["pred_inter_tensor"], g["pred_inter_tensor"]), "split-quad and quad-per-thread builds differ"
     assert eq(a["pred"], g["pred"])
+    assert eq(a["pred_inter_tensor"], h["pred_inter_tensor"]), "four- and two-thread split-quad builds differ"
+    assert eq(a["pred"], h["pred"])
     return a, b
 
 
@@ -135,7 +139,9 @@ def test_resident_engaged_at_c2():
             assert resident_config(8, 228, 304)[2] == 576
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
         ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in 13 x 19 parts of 72 quads,
-        assert ok and grid == 247 and block == 192          # two threads per quad (the split-quad build)
+        assert ok and grid == 247 and block == 320          # four threads per quad (a split-quad build)
+        with _env("2", "NLSPN_RES_SPLIT"):
+            assert resident_config(1, 228, 304)[2] == 192   # two threads per quad
         with _env("0", "NLSPN_RES_SPLIT"):
             assert resident_config(1, 228, 304)[2] == 128   # a thread per quad
         # C5 (1x17, fp16, 16 images): four groups of four images in 9 x 7 parts of 286 quads, two
