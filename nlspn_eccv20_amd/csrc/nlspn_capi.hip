@@ -50,6 +50,8 @@ extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kRe
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
+extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
+extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
@@ -389,10 +391,13 @@ template <typename T>
 const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first, int split = 0) {
     // the split-quad builds (3x3, `split` pixels per thread: 2 at 192 threads, 1 at 320; one
     // image group, step-1 form)
-    if (split)
-        return groups || first ? nullptr
-               : split == 1 ? reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>)
-                            : reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>);
+    if (split) {
+        if (groups || (first && split != 1)) return nullptr;
+        if (split == 1)
+            return first ? reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>)
+                         : reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>);
+        return reinterpret_cast<const void *>(&prop_resident_kernel<T, 3, 3, kResMaxNT, kResSMax, 192, false, false, 2>);
+    }
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
@@ -527,6 +532,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // setup work (27 raw planes, the normalisation's tanh / divisions) runs on two waves per
     // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
     // (profiles/r05/ab_first_r5f.json); C2 102.97 vs 107.52, C3 219.05 vs 227.37 the other way
+    const ResFirst *fp_split = fp;  // (the four-thread split build has a prologue form)
     if (S.nt <= 128) fp = nullptr;
     // Split quads: 3x3 parts of at most two waves in one image group (C1: 247 parts of 72
     // quads) run four threads per quad (320 threads) or two (192), cutting each thread's
@@ -544,7 +550,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
                 S.nt = ntc;
                 S.win_cells = cells;
                 row_bytes = rbs;
-                fp = nullptr;
+                fp = sp == 1 ? fp_split : nullptr;
             }
         }
     }

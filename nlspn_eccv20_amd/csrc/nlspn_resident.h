@@ -483,7 +483,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     constexpr int K = KH * KW - 1, REF = K / 2, PH = (KH - 1) / 2, PW = (KW - 1) / 2;
     constexpr int RY = res_ry(KH), RXQ = res_rxq(KW), PADX = kResPadX;
     constexpr int PX = PXO ? PXO : res_px(KH, KW), TPQ = 4 / PX;  // pixels per thread, threads per quad
-    static_assert(!(PXO && FIRST), "the split-quad builds run behind step 1");
     static_assert(PX == 1 || PX == 2 || PX == 4, "no resident form for this geometry");
     using RowV = typename RowT<PX>::type;
     constexpr unsigned ES = sizeof(T);
