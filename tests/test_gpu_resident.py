@@ -197,6 +197,25 @@ def test_resident_wide_geometry_bitexact(B, H, W, sigma, dtype, kernel, T):
     assert torch.equal(a["pred"], b["pred"])
 
 
+@pytest.mark.parametrize("B,H,W,sigma,dtype,kw,block", [
+    (1, 228, 304, 2.0, torch.float16, {}, 320),                         # C1 shape, fp16 storage
+    (1, 228, 304, 12.0, torch.float32, {"always_clip": True}, 320),     # fixed halo: the general path
+    (1, 228, 304, 2.0, torch.float32, {"preserve_input": False}, 320),
+    (2, 100, 120, 3.0, torch.float32, {"affinity": "TC"}, 320),
+    (1, 37, 52, 60.0, torch.float32, {}, None),                          # tiny, long ranges
+])
+def test_split_quad_builds_bitexact(B, H, W, sigma, dtype, kw, block):
+    """Small parts split their quads over four (or two) threads: bit-exact against the step
+    launches and the quad-per-thread build (_both), general path and fp16 included."""
+    with _env("1"):
+        ok, _, blk, _ = resident_config(B, H, W, 0 if dtype == torch.float32 else 1)
+        assert ok and (block is None or blk == block)
+    inp, _ = _inputs(B, H, W, sigma=sigma, dtype=dtype)
+    a, b = _both(inp, **kw)
+    assert torch.equal(a["pred_inter_tensor"], b["pred_inter_tensor"])
+    assert torch.equal(a["pred"], b["pred"])
+
+
 @pytest.mark.parametrize("T", [2, 3, 36])
 def test_resident_bitexact_short_and_long(T):
     inp, _ = _inputs(4, 64, 128, sigma=3.0)
