@@ -52,8 +52,6 @@ extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kRe
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
 extern template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
 extern template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
-extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
-extern template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 // defined in nlspn_kern_heads.hip
 #define NLSPN_HD_EXTERN(MB)                                            \
     extern template __global__ void heads_kernel<MB, true>(HeadsArgs); \
@@ -388,7 +386,7 @@ const void *res_fn_f(long long nt, bool groups) {
 
 // first: the build with the forward prologue and iteration 1 inside the launch (kResFirst)
 template <typename T>
-const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, bool first, int split = 0) {
+const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool first, int split = 0) {
     // the split-quad builds (3x3, `split` pixels per thread: 2 at 192 threads, 1 at 320; one
     // image group, step-1 form)
     if (split) {
@@ -401,10 +399,6 @@ const void *res_fn(int kh, long long nt, bool groups, bool pitch_ok, bool tail, 
     // the 576-thread builds have a compile-time window pitch (res_pitch): only when the
     // part's fixed-halo window fits it; otherwise the run-time-width build
     if (nt == 576 && !pitch_ok) nt = 0;
-    if (tail) {  // the eight-wave build (fp32 only; the planner checked its pitch; no prologue form)
-        if (groups) return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>);
-        return reinterpret_cast<const void *>(&prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>);
-    }
     // (the wider geometries: the step-1 form only, plan_resident)
     if (kh == 1) return first ? nullptr : res_fn_f<T, 1, 17, false>(nt, groups);
     if (kh == 5) return first ? nullptr : res_fn_f<T, 5, 5, false>(nt, groups);
@@ -513,21 +507,6 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     const int php = (H + S.gy - 1) / S.gy, pqp = (W / 4 + S.gx - 1) / S.gx;
     const bool pitch_ok = 4 * (pqp + 2 * rxq) + 2 * kResPadX <= res_pitch(576) &&
                           (php + 2 * ry) * res_pitch(576) <= res_build_cells(576, 576, K, px);
-    // The eight-wave build (nlspn_resident.h kResTailNT; fp32): parts of 449..576 quads
-    // (C2 541.5, C3 570), whose 512 threads own a quad each and the rest as tail pixels;
-    // its window has the same 128-cell pitch.  NLSPN_RES_TAIL=0 / 1 (A/B) forces the 576-thread
-    // build / this one there (bit-identical); unset: kResTailDefault.
-    const char *tenv = getenv("NLSPN_RES_TAIL");
-    const bool tail_on = tenv && (tenv[0] == '0' || tenv[0] == '1') ? tenv[0] == '1' : kResTailDefault;
-    const bool tail = dtype == NLSPN_DTYPE_F32 && tail_on && K == 8 && php * pqp > kResTailNT - 64 &&
-                      php * pqp <= kResTailNT + kResTailQuads &&
-                      4 * (pqp + 2 * kResRXQ) + 2 * kResPadX <= res_pitch(kResTailNT) &&
-                      (php + 2 * kResRY) * res_pitch(kResTailNT) <= kResTailWC;
-    if (tail) {
-        S.nt = kResTailNT;
-        S.win_cells = kResTailWC;
-        fp = nullptr;  // (the eight-wave build has no prologue form: step 1 runs before it)
-    }
     // Parts of two waves (a B=1 NYU image in 247 parts of 72 quads, C1): the prologue's
     // setup work (27 raw planes, the normalisation's tanh / divisions) runs on two waves per
     // CU, slower than step 1 across the whole chip: 93.5 vs 91.6 us per section same-process
@@ -539,7 +518,7 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     // latency-bound chain of tap-pixel slots from 32 to 8 or 16; NLSPN_RES_SPLIT=0 / 2 (A/B)
     // keeps a thread per quad / forces two
     int split = 0;
-    if (kh == 3 && S.nt <= 128 && !tail && B <= S.Bg) {
+    if (kh == 3 && S.nt <= 128 && B <= S.Bg) {
         const char *se = getenv("NLSPN_RES_SPLIT");
         const int want = se && (se[0] == '0' || se[0] == '2') ? se[0] - '0' : 1;
         for (int sp = want; sp >= 1 && sp <= 2 && !split; ++sp) {
@@ -570,13 +549,11 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     }
     P.first = fp != nullptr;
     // more than half a CU's LDS, so one workgroup per CU (a small part's window, capped at
-    // res_win_cells, may need less: the request is padded); the eight-wave build keeps
-    // conf' / dep planes and the tail pixels' planes instead of per-thread rows
-    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (tail ? (size_t)res_tail_rows_bytes() : (size_t)row_bytes * S.nt),
-                                        80 * 1024 + 16);
+    // res_win_cells, may need less: the request is padded)
+    const size_t lds = std::max<size_t>(4 * kResCtl + (size_t)S.win_cells * 8 + (size_t)row_bytes * S.nt, 80 * 1024 + 16);
     if (lds > (size_t)kResLds) return false;
-    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, false, pitch_ok, tail, P.first, split)
-                                    : res_fn<__half>(kh, S.nt, false, pitch_ok, false, P.first, split);
+    P.fn = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, false, pitch_ok, P.first, split)
+                                    : res_fn<__half>(kh, S.nt, false, pitch_ok, P.first, split);
     if (!P.fn) return false;
     P.block = (unsigned)S.nt;
     P.lds = lds;
@@ -586,13 +563,15 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
     unsigned dbg = 0;
     if (kExperiments)
         if (const char *d = getenv("NLSPN_RES_DBG")) dbg = (unsigned)atoi(d);
-    // Same-XCD hand-offs in the XCD's L2 (kResL2, nlspn_resident.h): possible where every
-    // image plane of every iteration starts and ends on a 128-B line (no line is shared
-    // by two images), not with the fused prologue; NLSPN_RES_L2=0 (A/B) keeps every
-    // hand-off write-through
+    // Per-line hand-offs (kResL2, nlspn_resident.h: a 128-B line no part on another XCC reads
+    // is stored plain and stays in its XCD's L2): possible where every image plane of every
+    // iteration starts and ends on a 128-B line (no line is shared by two images) and an
+    // image row holds at least a line (a line then spans at most two rows); NLSPN_RES_L2=0
+    // (A/B) exports every line (write-through)
     const char *l2env = getenv("NLSPN_RES_L2");
     const bool l2ok = !(l2env && l2env[0] == '0') && ((long long)HW * (long long)es) % 128 == 0 &&
-                      aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0;
+                      aligned(pred_inter, 128) && ((long long)B * HW * (long long)es) % 128 == 0 &&
+                      (long long)(W / 4) * 4 * (long long)es >= 128 && H < 65536 && W / 4 < 65536;
     const char *cenv = getenv("NLSPN_RES_OFFCOPY");
     const bool copy_off = off_out && !(flags & kResOffInserted) && !(cenv && cenv[0] == '0') &&
                           aligned(off_out, vb);
@@ -643,10 +622,13 @@ bool plan_resident(int dtype, const void *conf_eff, const void *dep, const void 
             }
     }
     if (nfull >= 2 && !(menv && menv[0] == '0') && !(dbg & 8u) && kh != 5) {
-        P.a[0].ngroups = nfull;
         // the group-loop build for the merged launch; a partial last group keeps the other
-        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, true, pitch_ok, tail, P.first)
-                                               : res_fn<__half>(kh, S.nt, true, pitch_ok, false, P.first);
+        P.fn_merged = dtype == NLSPN_DTYPE_F32 ? res_fn<float>(kh, S.nt, true, pitch_ok, P.first)
+                                               : res_fn<__half>(kh, S.nt, true, pitch_ok, P.first);
+        // (every merged shape has a GROUPS build; should one be missing, the groups launch
+        // one by one rather than a single-group build running only group 0)
+        if (!P.fn_merged) return true;
+        P.a[0].ngroups = nfull;
         int n = 1;
         if (ng > nfull) {  // the partial group, launched after the merged one
             P.a[1] = P.a[ng - 1];
@@ -665,6 +647,8 @@ int launch_resident(ResPlan &P, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent
     if (int rc = set_lds_attr(P.fn, (int)P.lds)) return rc;
     if (P.fn_merged)
         if (int rc = set_lds_attr(P.fn_merged, (int)P.lds)) return rc;
+    if (P.a[0].ngroups > 1 && !P.fn_merged)  // (plan_resident never makes one: a single-group build would run group 0 only)
+        return fail(NLSPN_EINVAL, "resident plan: %d merged image groups without a group-loop build", P.a[0].ngroups);
     for (int k = 0; k < P.ngroups; ++k) {
         const void *fn = k == 0 && P.fn_merged ? P.fn_merged : P.fn;
         if (g_rec)

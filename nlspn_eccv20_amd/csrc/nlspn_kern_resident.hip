@@ -33,8 +33,4 @@ template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 
 template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, false, 1>(ResArgs);
 template __global__ void prop_resident_kernel<float, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
 template __global__ void prop_resident_kernel<__half, 3, 3, kResMaxNT, kResSMax, 320, false, true, 1>(ResArgs);
-// the eight-wave build (kResTailNT: affinities in VGPRs, tail pixels; fp32), launch bound 512
-// (two waves per SIMD: 256 VGPRs per lane)
-template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, false, false>(ResArgs);
-template __global__ void prop_resident_kernel<float, 3, 3, kResTailNT, kResSMax, kResTailNT, true, false>(ResArgs);
 }  // namespace nlspn

@@ -33,10 +33,16 @@
 // is not the poison is this call's p_t: the consumer read the same producer's cells of
 // plane t - 1 one iteration earlier (the window and every tap are invariant, so a part
 // reads the same cells every iteration) and waited for them, and the producer had made
-// plane t's poison visible before it stored those (induction from plane 1).  Stores:
-// `sc1` (write-through; MI355X_MICROARCH.md § inter-workgroup visibility); an image whose
-// parts all run on one XCD (kResL2): plain, the lines stay in that XCD's L2.  Loads of p:
-// `sc1` (L1 bypassed).  Loads of bytes not written in this launch (conf', invariants) are
+// plane t's poison visible before it stored those (induction from plane 1).  Stores, per
+// 128-B line of a plane (kResL2, round 6): `sc1` (write-through; MI355X_MICROARCH.md
+// § inter-workgroup visibility) for an EXPORTED line — one that some part on another XCC
+// reads (its published window meets the line) — and plain for every other line, which then
+// stays in its XCD's L2 for the same-XCD readers.  Every part decides a line from the same
+// published words (the windows and XCC ids of its image's parts), so all the quads of a line
+// are stored the same way by whichever parts own them: a line is wholly L2-kept (producers
+// and readers on one XCD) or wholly write-through.  The decision is the same for every plane
+// of the call, so the induction above holds per line.  Without kResL2 every line is
+// exported.  Loads of p: `sc1` (L1 bypassed).  Loads of bytes not written in this launch (conf', invariants) are
 // plain.  Every plane is written once per call, so there is no write-after-read hazard, a
 // part never waits for a whole neighbour part (only for the cells it stages), and a fast
 // part may run ahead of parts that do not feed it.  Image groups run in turn inside one
@@ -116,34 +122,8 @@ struct ResArgs {
 typedef const __attribute__((address_space(4))) ResArgs ResArgsK;  // the kernarg segment's ResArgs
 
 constexpr int kResMaxNT = 768;                  // launch bound (threads per part)
-#ifndef NLSPN_RES_SMAX
-#define NLSPN_RES_SMAX 1
-#endif
-constexpr int kResSMax = NLSPN_RES_SMAX;         // staging quads per thread per round
-#ifndef NLSPN_RES_TAIL_SMAX
-#define NLSPN_RES_TAIL_SMAX 1
-#endif
-constexpr int kResTailSMax = NLSPN_RES_TAIL_SMAX;
-#ifndef NLSPN_RES_PRE
-#define NLSPN_RES_PRE 2
-#endif
-constexpr int kResPre = NLSPN_RES_PRE;  // the prologue's window staging: quads per thread in flight  // the same, eight-wave build (A/B builds: 2, 3)
-#ifndef NLSPN_RES_PF
-#define NLSPN_RES_PF 0
-#endif
-// tap-pixel slots whose LDS gathers are issued ahead of their arithmetic (A/B builds; 1-4
-// measured 3-5 % slower at C2 than the compiler's own schedule: the taps are bound by the
-// LDS array's bank-conflict cycles, not its latency, profiles/r04/ab_pf_r4b.txt)
-constexpr int kResPF = NLSPN_RES_PF;
-#ifndef NLSPN_RES_READ2
-#define NLSPN_RES_READ2 0  // A/B: let the two footprint rows merge into ds_read2st64_b64
-#endif
-#ifndef NLSPN_RES_EXP
-#define NLSPN_RES_EXP 0  // timing experiments only (tools/res_trace.py): 1 no gathers, 2 no tap arithmetic
-#endif
-#ifndef NLSPN_RES_FMA
-#define NLSPN_RES_FMA 0  // timing experiment only: contracted bilinear (not the oracle's arithmetic)
-#endif
+constexpr int kResSMax = 1;                      // staging quads per thread per round
+constexpr int kResPre = 2;                       // the prologue's window staging: quads per thread in flight
 #ifndef NLSPN_RES_SPIN_SLEEP
 #define NLSPN_RES_SPIN_SLEEP 1  // s_sleep between a staging spin's re-loads (A/B builds: 0, 2, 4)
 #endif
@@ -165,23 +145,12 @@ __host__ __device__ constexpr int res_px(int kh, int kw) {
 // bytes of a thread's LDS rows: the K affinities, 1 - sum, conf', dep of its PX pixels
 __host__ __device__ constexpr int res_row_bytes(int K, int px) { return (K + 3) * px * 4; }
 constexpr int kResPadX = 4;                      // zero columns either side of the window (keeps 16-B rows)
-constexpr int kResCtl = 8;                       // LDS control words ahead of the window
+// The export list (per-line write-through, below): at most kResNC foreign windows per part
+// (the parts on another XCC whose windows reach this part's 128-B lines), two words each
+constexpr int kResNC = 28;
+constexpr int kResCtl = 8 + 2 * kResNC;          // LDS control words ahead of the window
 constexpr int kResAS = 11;                       // float4 per thread (3x3): K = 8 affinities, 1 - sum, conf', dep
 constexpr int kResLds = 160 * 1024;              // LDS per CU
-
-// The eight-wave build (threads 512, fp32; round 5): two waves per SIMD instead of nine
-// waves over four SIMDs (one of which held three, the taps' VALU bound), the affinities,
-// the reference-tap weight, conf' and dep of the thread's quad in VGPRs instead of LDS rows
-// (256 VGPRs per lane at two waves per SIMD), and the part's quads beyond the 512 the threads
-// own as quads split into single TAIL pixels, one per lane of waves 4..7 (one wave of each
-// SIMD): a part of up to 576 quads (C2 541.5, C3 570) costs every SIMD at most 4 + 5 pixel-
-// slots of taps per iteration where the nine-wave build cost one SIMD 3 x 4.
-constexpr int kResTailNT = 512;
-constexpr bool kResTailDefault = false;          // (measured slower so far: opt-in, NLSPN_RES_TAIL=1)
-constexpr int kResTailQuads = 64;                // tail capacity: 4 waves x 64 lanes = 256 pixels
-// its LDS after the window: conf' and dep of every thread's quad (two float4 planes of NT,
-// structure of arrays: conflict-free), then the tail pixels' K + 3 values (planes of 256)
-__host__ __device__ constexpr int res_tail_rows_bytes() { return 16 * 2 * kResTailNT + 4 * (8 + 3) * 256; }
 
 // LDS cells per copy of the f window for nt threads: what the per-thread rows leave,
 // a multiple of 4 (16-B aligned copies), both copies addressable by 16-bit indices.
@@ -191,21 +160,17 @@ __host__ __device__ constexpr int res_win_cells(int nt, int row_bytes = 16 * kRe
                ? ((kResLds - 4 * kResCtl - row_bytes * nt) / 8 / 4 * 4)
                : cap;
 }
-// The eight-wave build keeps no per-thread rows: its two copies stay within 16-bit byte
-// addresses (4 * (kResCtl + 2 * 8,184) < 65,536).
-constexpr int kResTailWC = 8184;
 
 // the compile-time window pitch of a fixed-thread-count build (0: the pitch is the window's
 // width, a run-time value): 128 cells for 576 threads, whose two window copies span
-// 2 * 7,804 cells = 62.4 KB of byte addresses (below 64 KB: 16-bit), and for the eight-wave
-// build (2 * 8,184 cells)
-__host__ __device__ constexpr int res_pitch(int ntc) { return ntc == 576 || ntc == kResTailNT ? 128 : 0; }
+// 2 * 7,740 cells = 61.9 KB of byte addresses (below 64 KB: 16-bit)
+__host__ __device__ constexpr int res_pitch(int ntc) { return ntc == 576 ? 128 : 0; }
 // the window cells per copy of a build (threads ntc, 0: nt at run time) and geometry
 __host__ __device__ constexpr int res_build_cells(int ntc, int nt, int K, int px) {
-    return ntc == kResTailNT ? kResTailWC : res_win_cells(ntc ? ntc : nt, res_row_bytes(K, px), res_pitch(ntc) ? 8184 : 32764);
+    return res_win_cells(ntc ? ntc : nt, res_row_bytes(K, px), res_pitch(ntc) ? 8184 : 32764);
 }
 static_assert(4 * (kResCtl + 2 * res_win_cells(576)) < 65536, "576-thread window byte addresses need 16 bits");
-static_assert(4 * (kResCtl + 2 * kResTailWC) < 65536, "eight-wave window byte addresses need 16 bits");
+static_assert(kResCtl % 4 == 0, "the window starts 16-B aligned");
 
 constexpr unsigned kResSpinLimit = 1u << 22;     // ~seconds of polling before giving up
 #ifndef NLSPN_RES_NOGP
@@ -323,8 +288,7 @@ template <> struct ResVec<float> {
         const u32x4 q = {p, p, p, p};
         __builtin_amdgcn_raw_buffer_store_b128(q, r, vo, 0u, AUX);
     }
-    // one element (the eight-wave build's tail pixels: consecutive lanes, consecutive
-    // pixels, so a wave's dword stores coalesce)
+    // one element (PX = 1: the 5x5 build)
     template <unsigned AUX>
     static __device__ __forceinline__ void store1(rsrc_t r, unsigned vo, unsigned so, float v) {
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, AUX);
@@ -378,7 +342,7 @@ template <> struct ResVec<__half> {
         const u32x2 q = {w, w};
         __builtin_amdgcn_raw_buffer_store_b64(q, r, vo, 0u, AUX);
     }
-    // (the tail pixels are an fp32-only build: these exist for the shared kernel text)
+    // one element (PX = 1: the 5x5 build)
     template <unsigned AUX>
     static __device__ __forceinline__ void store1(rsrc_t r, unsigned vo, unsigned so, float v) {
         __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v), r, vo, so, AUX);
@@ -470,8 +434,7 @@ template <int PX> __device__ __forceinline__ void win_put(float *fwin, float *fw
 
 // 3x3 geometry (K = 8, prop_kernel 3, the reference default), raw offset layout.
 // MAXNT = launch bound (threads), SMAX = staging quads per thread per round.
-// NTC = the thread count as a compile-time constant (0: blockDim.x at run time);
-// NTC = kResTailNT (512): the eight-wave build (affinities in VGPRs, tail pixels).
+// NTC = the thread count as a compile-time constant (0: blockDim.x at run time).
 // GROUPS: runs ResArgs::ngroups image groups in turn (false: one; the group loop then
 // folds away, and with it the setup spill slots it costs).
 // KH x KW: the tap geometry; PX = res_px(KH, KW) pixels per thread (4: a quad per thread).
@@ -507,13 +470,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // across lanes): the K affinities, 1 - sum, the own pixels' conf' (1 with conf_prop off)
     // and dep (0 with preserve off) — every one an immediate offset from ONE address register.
     RowV *akl = reinterpret_cast<RowV *>(fwinB + WC) + (size_t)tid * (K + 3);
-    // the eight-wave build: the quad's affinities and 1 - sum in VGPRs (aq), its conf' / dep
-    // in two float4 planes of NT (cdl), the tail pixels' values in K + 3 planes of 256 (tal)
-    constexpr bool TAIL = NTC == kResTailNT;
-    static_assert(!TAIL || (K == 8 && PX == 4), "the eight-wave build is 3x3 quads");
-    constexpr int SM = TAIL ? kResTailSMax : SMAX;  // staging quads per thread per round
-    float4 *cdl = reinterpret_cast<float4 *>(fwinB + WC);
-    float *tal = reinterpret_cast<float *>(cdl + 2 * NT) + (tid - 256);
+    constexpr int SM = SMAX;  // staging quads per thread per round
 
     gu32 *sync = (gu32 *)(a.sync);
     const int ngroups = GROUPS && a.ngroups > 1 ? a.ngroups : 1;
@@ -566,23 +523,23 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         res_wtrace(a.pred, a.T, __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u), -1)[0] = hw;
     }
-    // TAIL: the threads own the part's first NT quads as quads, the rest as tail pixels (below)
-    const int nq_main = TAIL ? min(nown, NT) : nown;
+    const int nq_main = nown;
     const bool active = tid < nq_main;
     // Every part publishes, once its setup is done, the XCC it runs on, tagged with the image
     // group (grp + 1, above the 5-bit XCC field; the words start every launch at zero,
     // res_finish), and iteration 1 of the group waits until every part of its image has
     // published a tag of this group or a later one.  Two uses:
-    //  * same-XCD hand-offs (flags kResL2, host: plane layout line-aligned): if all parts of
-    //    the image share one XCC, the image's hand-offs stay in that XCD's L2 (below).
-    //    Placement is read, never assumed;
+    //  * per-line hand-offs (flags kResL2, host: plane layout line-aligned): beside the tag a
+    //    part publishes its in-image window (the cells it stages; with the fixed halo, whose
+    //    general path reads any cell, the whole image), and a line is exported iff a part on
+    //    another XCC has a window meeting it (above).  Placement is read, never assumed;
     //  * the prologue in the launch (kResFirst): a part publishes only after its stores of
     //    conf' and of plane 0's poison are acknowledged, so a consumer that has seen every tag
     //    of its image reads neither a previous call's conf' nor its plane 0 (the sc1 row of
     //    MI355X_MICROARCH.md's hand-off table: sc1 stores, every storing wave's vmcnt(0) and a
     //    workgroup barrier before the tag, sc1 loads behind the poll and a barrier).
     const bool l2try = (a.flags & kResL2) != 0;
-    constexpr bool first = FIRST && !TAIL;  // (the eight-wave build: no prologue form)
+    constexpr bool first = FIRST;
     const bool publish = l2try || first;
     unsigned xcc_self = 0;
     const unsigned xtag = (unsigned)(grp + 1) << 5;
@@ -590,12 +547,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         unsigned x;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
         xcc_self = (x & 0xfu) + 1u;
-        // after a step-1 launch the tag only carries the placement: published at once (the
-        // prologue form publishes after its stores, below the window pass)
-        if (!first && tid == 0)
-            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
     }
+    // this part's sync line: word 1 the tag, words 2 + 2 (grp & 1) and 3 + 2 (grp & 1) the
+    // window of group grp (two slots: a part publishes group g + 1 while a slower part of its
+    // image may still read group g's; it cannot reach group g + 2 before that part has
+    // published g + 1, which the t = 1 wait of g + 1 needs)
+    gu32 *const myline = &sync[kResLine * (1 + blockIdx.x)];
     const float Hf = (float)H, Wf = (float)W;
     int y = r0, x0 = 4 * c0;
     if (active) {  // quad tid / TPQ of the part (row-major), pixels (tid % TPQ) * PX .. + PX - 1 of it
@@ -604,25 +561,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         x0 = 4 * (c0 + q - rr * nqw) + (TPQ == 1 ? 0 : (tid % TPQ) * PX);
     }
     const unsigned vpix = (unsigned)(y * W + x0) * ES;
-    // ---- TAIL: pixel tj of the quads beyond the first NT (row-major in the part), one per
-    // lane of waves 4..7 — one wave of each SIMD — in four contiguous chunks (consecutive
-    // lanes hold consecutive pixels, so the wave's dword stores coalesce)
-    const int ntail = TAIL ? 4 * (nownq - nq_main) : 0;
-    const int tchunk = (ntail + 3) >> 2;
-    const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave (uniform)
-    const int tj = (wvu - 4) * tchunk + lane;
-    const bool tail_on = TAIL && wvu >= 4 && lane < tchunk && tj < ntail;
-    const bool tail_wave = TAIL && wvu >= 4 && (wvu - 4) * tchunk < ntail;  // wave-uniform
-    int ty = r0, tx = 4 * c0;
-    if (tail_on) {
-        const int q = NT + (tj >> 2), rr = q / nqw;
-        ty = r0 + rr;
-        tx = 4 * (c0 + q - rr * nqw) + (tj & 3);
-    }
-    const unsigned tvpix = (unsigned)(ty * W + tx) * ES;
     float hy[K][PX], hx[K][PX];
-    float4 aq[K + 1];          // TAIL: the quad's affinities and 1 - sum (what akl holds otherwise)
-    float thy[K] = {}, thx[K] = {};  // TAIL: the tail pixel's sample coordinates
     // the quad's affinities, dep and conf (with the prologue in the launch: raw, processed after
     // the geometry pass below, so that pass runs while they stream in)
     float ak[K][PX], dv[PX], cq[PX];
@@ -684,44 +623,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         }
         // the affinities are consumed last in a tap, so they wait in LDS (conflict-
         // free 16-B rows per thread) and leave the registers to the tap coordinates
-        // (the eight-wave build: in VGPRs, two waves per SIMD leave 256 per lane)
-        if constexpr (TAIL) {  // (PX = 4)
 #pragma unroll
-            for (int k = 0; k < K; ++k) aq[k] = rv_make<PX>(ak[k]);
-            aq[K] = rv_make<PX>(aref);
-            cdl[tid] = rv_make<PX>(cq);
-            cdl[NT + tid] = rv_make<PX>(dv);
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k) akl[k] = rv_make<PX>(ak[k]);
-            if (!first) akl[K] = rv_make<PX>(aref);
-            akl[K + 1] = rv_make<PX>(cq);
-            akl[K + 2] = rv_make<PX>(dv);
-        }
-        if (TAIL && wvu >= 4) {  // the tail pixel's invariants (lanes without one load pixel (r0, 4 c0): unused)
-            float taf[K + 3];
-            float s = 0.f;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                taf[k] = ResVec<T>::template load1<0>(ra_, tvpix, (unsigned)(k < REF ? k : k + 1) * plane_bytes);
-                const int ok = (off_ins && k >= REF) ? k + 1 : k;
-                thy[k] = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)(2 * ok) * plane_bytes);
-                thx[k] = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)(2 * ok + 1) * plane_bytes);
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) s += taf[k];
-            taf[K] = 1.0f - s;
-            taf[K + 1] = has_conf ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.conf) + b * HW), tvpix, 0u) : 1.f;
-            taf[K + 2] = preserve ? ResVec<T>::template load1<0>(make_rsrc(static_cast<const T *>(a.dep) + b * HW), tvpix, 0u) : 0.f;
-#pragma unroll
-            for (int k = 0; k < K + 3; ++k) tal[256 * k] = taf[k];
-        }
+        for (int k = 0; k < K; ++k) akl[k] = rv_make<PX>(ak[k]);
+        if (!first) akl[K] = rv_make<PX>(aref);
+        akl[K + 1] = rv_make<PX>(cq);
+        akl[K + 2] = rv_make<PX>(dv);
     }
     // the prologue: the affinity normalisation with the reference-tap weight 1 - sum
     // (nlspn_common.h normalize_taps, step 1's IEEE sequence), one pixel of the quad at a time
     // from the raw values in the LDS rows (a rolled loop: the 4 x K values of the quad at once
     // cost the GROUPS builds scratch)
-    if constexpr (!TAIL) {
+    {
         if (first) {
             const float gamma = *a.gamma;
 #pragma unroll 1
@@ -752,10 +664,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     }
     if (trace0 && tid == 0) trace0[4] = __builtin_amdgcn_s_memrealtime();  // (the prologue's normalisation done)
     // the own pixels' row k (affinity k < K, K: 1 - sum, K + 1: conf', K + 2: dep)
-    const auto aff4 = [&](const int k) -> RowV {
-        if constexpr (TAIL) return k <= K ? aq[k < K + 1 ? k : 0] : cdl[(k - K - 1) * NT + tid];
-        else return akl[k];
-    };
+    const auto aff4 = [&](const int k) -> RowV { return akl[k]; };
 
     // ---- the window: the rectangle of every cell a valid tap of this part touches
     // (offsets are invariant, so once), when it fits the LDS cells allocated;
@@ -809,22 +718,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 wmx = fmaxf(wmx, ok ? w_im : -__builtin_inff());
             }
         }
-        if (TAIL) {  // the tail pixel's taps
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int t = k < REF ? k : k + 1, i = t / KW, jj = t % KW;
-                const float h_im = (float)(ty - PH + i) + thy[k];
-                const float w_im = (float)(tx - PW + jj) + thx[k];
-                thy[k] = h_im;
-                thx[k] = w_im;
-                if (tail_on && h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                    hmn = fminf(hmn, h_im);
-                    hmx = fmaxf(hmx, h_im);
-                    wmn = fminf(wmn, w_im);
-                    wmx = fmaxf(wmx, w_im);
-                }
-            }
-        }
         int mn = r0, mx = r1, cmn = 4 * c0, cmx = 4 * c1;
         if (hmn <= hmx) {
             mn = min(mn, (int)floorf(hmn));
@@ -832,7 +725,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             cmn = min(cmn, (int)floorf(wmn));
             cmx = max(cmx, (int)floorf(wmx) + 1);
         }
-        res_span_merge(ctl, active || tail_on, mn, mx, cmn, cmx);
+        res_span_merge(ctl, active, mn, mx, cmn, cmx);
     }
     lds_barrier();
     int rlo = ctl[1], rhi = ctl[2], wq0 = ctl[3] >> 2, wq1 = ctl[4] >> 2;  // >> 2: floor for negatives too
@@ -852,8 +745,21 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     const int ra = max(rlo, 0), rb = min(rhi, H - 1);      // in-image window rows
     const int qa = max(wq0, 0), qb = min(wq1, W4 - 1);     // in-image window quad columns
     const int wqn = qb - qa + 1;
+    // the window as published (16-bit fields): the in-image cells this part reads of other
+    // parts' planes; the fixed halo's general path reads any cell: the whole image
+    const unsigned pw0 = dynwin ? (unsigned)ra | ((unsigned)rb << 16) : ((unsigned)(H - 1) << 16);
+    const unsigned pw1 = dynwin ? (unsigned)qa | ((unsigned)qb << 16) : ((unsigned)(W4 - 1) << 16);
+    if (l2try && tid == 0) {
+        __hip_atomic_store(&myline[2 + 2 * (grp & 1)], pw0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&myline[3 + 2 * (grp & 1)], pw1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // after a step-1 launch the tag carries the placement and the window: published now (its
+    // words acknowledged first); the prologue form publishes after its stores, below
+    if (publish && !first && tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&myline[1], xtag | xcc_self, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     lds_barrier();
-    if (tid == 0) { ctl[1] = ra; ctl[2] = rb; ctl[3] = 4 * qa; ctl[4] = 4 * qb + 3; }
     for (int i = tid; i < WH * WW; i += NT) fwin[i] = fwinB[i] = 0.f;  // cells outside the image stay 0
     lds_barrier();
     if (trace0 && tid == 0) trace0[2] = __builtin_amdgcn_s_memrealtime();
@@ -898,24 +804,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
     }
-    bool has_fb_t = false;  // TAIL: the tail pixel has a tap outside the window
-    if (TAIL) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float h_im = thy[k], w_im = thx[k];
-            if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
-                if (!((unsigned)(h_low - rlo) < (unsigned)(WH - 1) && (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)))
-                    has_fb_t = true;
-            } else {
-                thy[k] = (float)rlo;
-                thx[k] = (float)(4 * wq0 - PADX);
-            }
-        }
-        has_fb_t = has_fb_t && tail_on && !dynwin;
-    }
     if (trace0 && tid == 0) trace0[3] = __builtin_amdgcn_s_memrealtime();
-    const bool wave_fb = __ballot(has_fb || has_fb_t) != 0;  // wave-uniform: this wave has general-path lanes
+    const bool wave_fb = __ballot(has_fb) != 0;  // wave-uniform: this wave has general-path lanes
     // Every tap's bilinear geometry is iteration-invariant, so it is resolved once:
     // the fractional parts lh = h - floor(h), lw = w - floor(w) (.cuh:35-36, the same
     // values the per-iteration form computes) and the window cell of the footprint's
@@ -947,27 +837,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 adp[sl >> 1] |= idx << (16 * (sl & 1));
             }
         }
-    }
-
-    float tlh[K], tlw[K];  // TAIL: the tail pixel's tap geometry (the same resolution)
-    unsigned tadp[K / 2];
-    int town = 0;          // TAIL: window cell of the tail pixel
-    if (TAIL) {
-        const float WWf = (float)WW;
-        const int lbase = PADX - 4 * wq0 - rlo * WW, bofs = WC - 1;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float fh = floorf(thy[k]), fw = floorf(thx[k]);
-            tlh[k] = thy[k] - fh;
-            tlw[k] = thx[k] - fw;
-            int li = (int)(fh * WWf + fw) + lbase;
-            li = ((unsigned)li < (unsigned)(WH * WW)) ? li : 0;
-            unsigned idx = (li & 1) ? (unsigned)(li + bofs) : (unsigned)li;
-            idx = 4u * ((unsigned)kResCtl + idx);  // (a PITCH build: LDS byte addresses)
-            if (k & 1) tadp[k >> 1] |= idx << 16;
-            else tadp[k >> 1] = idx;
-        }
-        town = (ty - rlo) * WW + tx - 4 * wq0 + PADX;
     }
 
     // Staging map (iterations t >= 2): the in-image window quads outside the own
@@ -1035,13 +904,11 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
         }
         if (__builtin_amdgcn_ballot_w64(nonfin) != 0 && lane == 0) ctl[6] = 1;  // iteration 0's flag
-        // the prologue's conf' and plane-0 poison stores acknowledged by every wave, then a
-        // barrier, then the part publishes (the hand-off table's sc1 row)
+        // the prologue's conf' and plane-0 poison stores (and tid 0's window words) acknowledged
+        // by every wave, then a barrier, then the part publishes (the hand-off table's sc1 row)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (tid == 0)
-            __hip_atomic_store(&sync[kResLine * (1 + blockIdx.x) + 1], xtag | xcc_self, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store(&myline[1], xtag | xcc_self, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // Iteration t reads plane t-1 and writes plane t: t = 1 .. T-1 (the section's iterations
@@ -1050,7 +917,14 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
     // staged above.  The XCC ids are read by the last wave holding quads (any wave would do).
     const int t0 = first ? 0 : 1;
     const int pwave = (nq_main - 1) >> 6;
-    bool l2 = false;  // this image's hand-offs stay in the XCD's L2 (set in iteration 1)
+    // this thread's quad's line is exported (sc1 stores); decided in iteration 1, before
+    // that (the prologue form's plane 0 and plane-1 poison) every line is.  The small-part
+    // builds export every line: the fp32 128-thread build (read-ahead taps at the 168-VGPR
+    // cap) paid a scratch reload in its iteration loop for the per-lane flag, and the split
+    // builds (C1: 247 parts over all eight XCDs, most lines read across XCDs anyway) measured
+    // 10 % slower with it (55.1 vs 50.1 us per section same process, profiles/r06)
+    constexpr bool LINES = !(NTC == 128 || PXO != 0);
+    bool ex = true;
     const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);  // first thread of this wave
     int t_abort = 0;
     for (int t = t0; t < a.T; ++t) {
@@ -1070,25 +944,31 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         const bool cpy = !OFFSETUP && a.off_out != nullptr && cpc < 2 * (K + 1);
         const int cptt = cpc >> 1;
         const int cpsrc = cptt == REF ? -1 : 2 * (cptt < REF ? cptt : cptt - 1) + (cpc & 1);
-        float cpq[PX], cpq1 = 0.f;
+        float cpq[PX];
 #pragma unroll
         for (int e = 0; e < PX; ++e) cpq[e] = 0.f;
         if (cpy && cpsrc >= 0) {
             const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
             if (active) PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)cpsrc * plane_bytes, cpq);
-            if (tail_on) cpq1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)cpsrc * plane_bytes);
         }
         // ---- iteration 1, the first to read other parts' cells: wait until every part of the
-        // image has published this group's tag (or a later group's); then the hand-off mode of
-        // this image (all its parts on this part's XCC: L2), decided from the published XCC
-        // ids, identically by every part of the image; its stores use it.  With the prologue
+        // image has published this group's tag (or a later group's).  Then the export list: the
+        // published windows of the image's parts on ANOTHER XCC that can meet a line holding one
+        // of this part's quads (rows r0 - 1 .. r1: a line spans at most two rows; columns within
+        // a line of the own ones, or every column for a part at a row's start or end, whose
+        // lines wrap), into LDS (ctl[8 ..], ctl[5] their count; -1: every line exported — no
+        // per-line mode, a timed-out wait, or more than kResNC such windows).  With the prologue
         // in the launch a timed-out wait aborts (the conf' and plane 0 it guards are unknown).
+        constexpr int LQ = 128 / (4 * (int)ES);  // quads per 128-B line
         if (t == 1) {
             if ((tid >> 6) == pwave) {
-                bool same = l2try, fail = false;
+                bool fail = false, ovf = false;
+                int nc = 0;  // (wave-uniform)
                 unsigned spins = 0;
-                // (after a step-1 launch only the placement is read: done at the first other XCC)
-                for (int base = 0; publish && base < nparts && !fail && (first || same); base += 64) {
+                const int er0 = r0 - 1, er1 = r1;
+                const bool wrap = c0 == 0 || c1 == W4;
+                const int ec0 = wrap ? 0 : c0 - LQ, ec1 = wrap ? W4 - 1 : c1 - 1 + LQ;
+                for (int base = 0; publish && base < nparts && !fail; base += 64) {
                     const int jj = base + lane;
                     gu32 *wp = &sync[kResLine * (1 + xcd_unmap(bl * nparts + (jj < nparts ? jj : 0), G)) + 1];
                     unsigned v;
@@ -1102,10 +982,23 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    same = same && __all((v & 31u) == xcc_self);
+                    if (l2try && !fail) {  // (the window words were acknowledged before the tag)
+                        const unsigned w0 = __hip_atomic_load(wp + 1 + 2 * (grp & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned w1 = __hip_atomic_load(wp + 2 + 2 * (grp & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const bool cand = jj < nparts && (v & 31u) != xcc_self && (int)(w0 & 0xffffu) <= er1 &&
+                                          (int)(w0 >> 16) >= er0 && (int)(w1 & 0xffffu) <= ec1 && (int)(w1 >> 16) >= ec0;
+                        const unsigned long long m = __builtin_amdgcn_ballot_w64(cand);
+                        const int at = nc + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                        if (cand && at < kResNC) {
+                            ctl[8 + 2 * at] = (int)w0;
+                            ctl[9 + 2 * at] = (int)w1;
+                        }
+                        nc += __builtin_popcountll(m);
+                        ovf = ovf || nc > kResNC;
+                    }
                 }
                 if (lane == 0) {
-                    ctl[5] = same && !fail ? 1 : 0;
+                    ctl[5] = (!l2try || fail || ovf) ? -1 : nc;
                     if (fail && first) {
                         ctl[0] = 1;
                         __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1114,7 +1007,23 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 }
             }
             lds_barrier();
-            l2 = __builtin_amdgcn_readfirstlane(ctl[5]) != 0;
+            // this quad's line: flat quad range [lq, lq + LQ) of the plane (planes start on a line,
+            // host), row ya from column ca, wrapping into row ya + 1 when it passes the row's end
+            const int nc = __builtin_amdgcn_readfirstlane(ctl[5]);
+            if (LINES && nc >= 0) {
+                // (the own quad's row and column recomputed from its byte offset: not live across the loop)
+                const int pe = (int)(vpix / ES), yq = pe / W, fq = pe >> 2, lq = fq & ~(LQ - 1);
+                const int ya = lq < yq * W4 ? yq - 1 : yq, ca = lq - ya * W4, ce = ca + LQ - 1;
+                const int ca1 = min(ce, W4 - 1), cb1 = ce - W4;  // cb1 >= 0: columns 0..cb1 of row ya + 1
+                bool hit = false;
+                for (int i = 0; i < nc; ++i) {
+                    const unsigned w0 = (unsigned)ctl[8 + 2 * i], w1 = (unsigned)ctl[9 + 2 * i];
+                    const int wr0 = (int)(w0 & 0xffffu), wr1 = (int)(w0 >> 16), wc0 = (int)(w1 & 0xffffu), wc1 = (int)(w1 >> 16);
+                    hit = hit || (ya >= wr0 && ya <= wr1 && ca <= wc1 && ca1 >= wc0) ||
+                          (cb1 >= 0 && ya + 1 >= wr0 && ya + 1 <= wr1 && wc0 <= cb1);
+                }
+                ex = hit;
+            }
         }
         if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
 
@@ -1208,20 +1117,17 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         if (cpy) {  // streaming (nt): an output only
             const rsrc_t rco = make_rsrc(static_cast<T *>(a.off_out) + (long long)b * 2 * (K + 1) * HW);
             if (active) PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)cpc * plane_bytes, cpq);
-            if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)cpc * plane_bytes, cpq1);
             if (t == a.T - 1) {  // a short section: the planes past T - 1, here
                 const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
                 for (int c = cpc + 1; c < 2 * (K + 1); ++c) {
                     const int tt = c >> 1, src = tt == REF ? -1 : 2 * (tt < REF ? tt : tt - 1) + (c & 1);
-                    float q[PX], q1 = 0.f;
+                    float q[PX];
 #pragma unroll
                     for (int e = 0; e < PX; ++e) q[e] = 0.f;
                     if (src >= 0) {
                         if (active) PixVec<T, PX>::template load<0>(ro, vpix, (unsigned)src * plane_bytes, q);
-                        if (tail_on) q1 = ResVec<T>::template load1<0>(ro, tvpix, (unsigned)src * plane_bytes);
                     }
                     if (active) PixVec<T, PX>::template store<kNT>(rco, vpix, (unsigned)c * plane_bytes, q);
-                    if (tail_on) ResVec<T>::template store1<kNT>(rco, tvpix, (unsigned)c * plane_bytes, q1);
                 }
             }
         }
@@ -1232,12 +1138,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
         // plane t + 1 is read by iteration t + 2 (if any): its own quad poisoned now, the
         // store acknowledged before plane t's store below (the hand-off's ordering)
         if (active && t + 2 < a.T) {
-            if (l2) PixVec<T, PX>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
-            else PixVec<T, PX>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
-        }
-        if (tail_on && t + 2 < a.T) {
-            if (l2) ResVec<T>::template poison1<0>(make_rsrc(p_out + a.tstride), tvpix);
-            else ResVec<T>::template poison1<kSc1>(make_rsrc(p_out + a.tstride), tvpix);
+            if (ex) PixVec<T, PX>::template poison<kSc1>(make_rsrc(p_out + a.tstride), vpix);
+            else PixVec<T, PX>::template poison<0>(make_rsrc(p_out + a.tstride), vpix);
         }
 
         // ---- taps (prop_step_kernel's arithmetic, accumulated in tap-index order)
@@ -1250,11 +1152,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             for (int e = 0; e < PX; ++e) asm volatile("" : "+v"(lhv[k][e]), "+v"(lwv[k][e]));
 #pragma unroll
             for (int i = k * PX / 2; i < (k + 1) * PX / 2; ++i) asm volatile("" : "+v"(adp[i]));
-            if (TAIL) asm volatile("" : "+v"(tlh[k]), "+v"(tlw[k]));
         }
-        if (TAIL)
-#pragma unroll
-            for (int k = 0; k < K / 2; ++k) asm volatile("" : "+v"(tadp[k]));
         float pown[PX];  // p_t of the own pixels, as stored
 #pragma unroll
         for (int e = 0; e < PX; ++e) pown[e] = 0.f;
@@ -1292,64 +1190,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
             return has_conf ? pv * ResVec<T>::template load1<kSc1>(rcg, qo, 0u) : pv;
         };
-        // Affinity k and 1 - sum from LDS (arow[k * astep], arow[K * astep]), or, with arow null
-        // (the eight-wave build's quads: their rows are in VGPRs), re-read from global memory.
-        const auto gp_pixel = [&](const int gy, const int gx, const int lcell, const unsigned gvo, const float *arow,
-                                  const int astep) -> float {
-            const rsrc_t ro = make_rsrc(static_cast<const T *>(a.off) + (long long)b * a.off_bs);
-            const rsrc_t rg = make_rsrc(static_cast<const T *>(a.aff) + (long long)b * (K + 1) * HW);
-            const bool glb = TAIL && arow == nullptr;
-            float s = 0.f;
-#pragma unroll 1
-            for (int k = 0; k < K; ++k) {
-                if (k == REF) {
-                    float ar;
-                    if (glb) {
-                        float sa = 0.f;
-#pragma unroll 1
-                        for (int k2 = 0; k2 < K; ++k2)
-                            sa += ResVec<T>::template load1<0>(rg, gvo, (unsigned)(k2 < REF ? k2 : k2 + 1) * plane_bytes);
-                        ar = 1.0f - sa;
-                    } else {
-                        ar = arow[K * astep];
-                    }
-                    s += fwin[lcell] * ar;
-                }
-                const float av = glb ? ResVec<T>::template load1<0>(rg, gvo, (unsigned)(k < REF ? k : k + 1) * plane_bytes)
-                                     : arow[k * astep];
-                const int tt = k < REF ? k : k + 1, i = tt / KW, jj = tt % KW;
-                const int ok = (off_ins && k >= REF) ? k + 1 : k;
-                const float h_im = (float)(gy - PH + i) + ResVec<T>::template load1<0>(ro, gvo, (unsigned)(2 * ok) * plane_bytes);
-                const float w_im = (float)(gx - PW + jj) + ResVec<T>::template load1<0>(ro, gvo, (unsigned)(2 * ok + 1) * plane_bytes);
-                float v = 0.f;
-                if (h_im > -1.f && w_im > -1.f && h_im < Hf && w_im < Wf) {
-                    const int h_low = (int)floorf(h_im), w_low = (int)floorf(w_im);
-                    const float lh = h_im - (float)h_low, lw = w_im - (float)w_low;
-                    const float hh = 1.f - lh, hw = 1.f - lw;
-                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    if ((unsigned)(h_low - rlo) < (unsigned)(WH - 1) && (unsigned)(w_low - 4 * wq0) < (unsigned)(WWp - 1)) {
-                        const float *sp = &fwin[(h_low - rlo) * WW + w_low - 4 * wq0 + PADX];
-                        v = (w1 * sp[0] + w2 * sp[1] + w3 * sp[WW] + w4 * sp[WW + 1]);
-                    } else {
-                        const int h_high = h_low + 1, w_high = w_low + 1;
-                        float c4[4];
-                        const int cy[4] = {h_low, h_low, h_high, h_high};
-                        const int cx[4] = {w_low, w_high, w_low, w_high};
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            c4[u] = 0.f;
-                            if (cy[u] >= 0 && cy[u] <= H - 1 && cx[u] >= 0 && cx[u] <= W - 1) {
-                                const unsigned qo = (unsigned)(cy[u] * W + cx[u]) * ES;
-                                c4[u] = gp_corner(qo);
-                            }
-                        }
-                        v = (w1 * c4[0] + w2 * c4[1] + w3 * c4[2] + w4 * c4[3]);
-                    }
-                }
-                s += v * av;
-            }
-            return s;
-        };
         const auto gp_raise = [&]() {  // a general-path spin timed out: the abort (rare lanes)
             if (gp_fail) {
                 ctl[0] = 1;
@@ -1357,37 +1197,21 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         };
-        // TAIL: the tail pixel's taps (tail waves: lanes with a tail pixel), after the quad's
-        // (its reads interleaved into the quad's slot loop spilled: 256 VGPRs + 64 in scratch)
-        float tacc = 0.f;
-        const auto tail_tap = [&](const int k) {
-            if (k == REF) tacc += fwin[town] * tal[256 * K];
-            const unsigned idx = (k & 1) ? (tadp[k >> 1] >> 16) : (tadp[k >> 1] & 0xffffu);
-            const float2 s01 = lds_pair(idx);
-            __builtin_amdgcn_sched_barrier(0);
-            const float2 s23 = lds_pair(idx + 4u * PITCH);
-            const float lh = tlh[k], lw = tlw[k];
-            const float hh = 1.f - lh, hw = 1.f - lw;
-            const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-            const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
-            tacc += v * tal[256 * k];
-        };
         if (active && !(exp_dbg(a.dbg) & 4u)) {
             float acc[PX];
 #pragma unroll
             for (int e = 0; e < PX; ++e) acc[e] = 0.f;
             // branch-free path: every tap from the LDS window (invalid taps read zeros), in
-            // K PX tap-pixel slots s = PX k + e (3x3 quads: 32).  kResPF > 0 (A/B builds) issues slot s + PF's two
-            // footprint reads before slot s's arithmetic; the default leaves the schedule to
-            // the compiler (waits per slot), which measured faster: nine waves per CU already
-            // keep the LDS array busy, and its bank-conflict cycles, not the read latency,
-            // bound the taps (profiles/r04).  Same arithmetic, same order per pixel either way.
-            // 128-thread builds (small parts, e.g. C1's 247 of 72 quads: two waves, the taps one
-            // wave's dependency chain) issue the reads 4 slots ahead: C1 +3.9 % same-box; the
-            // 576-thread builds (nine waves keep the LDS busy) lose 4 % with it
-            // (profiles/r04/ab_pf_r4s_*.txt)
-            // (fp32: the fp16 build spills with it)
-            constexpr int PF = ((NTC == 128 || PXO != 0) && kResPF == 0 && ES == 4) ? 4 : kResPF;
+            // K PX tap-pixel slots s = PX k + e (3x3 quads: 32).  The large builds leave the
+            // schedule to the compiler (waits per slot): nine waves per CU already keep the LDS
+            // array busy, and its bank-conflict cycles, not the read latency, bound the taps
+            // (issuing 1-4 slots ahead measured 3-5 % slower at C2, profiles/r04/ab_pf_r4b.txt).
+            // 128-thread and split-quad builds (small parts, e.g. C1's 247 of 72 quads: two
+            // waves, the taps one wave's dependency chain) issue slot s + PF's two footprint
+            // reads before slot s's arithmetic, PF = 4: C1 +3.9 % same-box
+            // (profiles/r04/ab_pf_r4s_*.txt; fp32: the fp16 build spills with it).  Same
+            // arithmetic, same order per pixel either way.
+            constexpr int PF = ((NTC == 128 || PXO != 0) && ES == 4) ? 4 : 0;
             float2 g01[NSL], g23[NSL];
             RowV akv[K + 1];
             RowV cref;  // the reference tap's own-pixel cells (one-cell form; the four-corner
@@ -1400,28 +1224,18 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                     cref = *reinterpret_cast<const RowV *>(&fwin[lown]);
                 }
                 const unsigned idx = (s & 1) ? (adp[s >> 1] >> 16) : (adp[s >> 1] & 0xffffu);
-#if NLSPN_RES_EXP == 1  // timing experiment: no gathers (wrong results)
-                g01[s] = make_float2(__builtin_bit_cast(float, idx), 1.f);
-                g23[s] = make_float2(2.f, __builtin_bit_cast(float, idx + 1u));
-#else
                 if constexpr (PITCH != 0) {  // an LDS byte address (the dynamic LDS starts at 0)
                     g01[s] = lds_pair(idx);
-#if NLSPN_RES_READ2
-                    // the compiler merges the two rows into one ds_read2st64_b64
-                    g23[s] = lds_pair(idx + 4u * PITCH);
-#else
                     // two ds_read_b64 (one address register, the lower row an immediate offset):
                     // ds_read2st64_b64, what the compiler would merge the pair into, runs at
                     // half the LDS rate (16-lane groups, MI355X_MICROARCH.md LDS table); a
                     // scheduling barrier keeps them apart
                     __builtin_amdgcn_sched_barrier(0);
                     g23[s] = lds_pair(idx + 4u * PITCH);
-#endif
                 } else {
                     g01[s] = *reinterpret_cast<const float2 *>(fwin + idx);
                     g23[s] = *reinterpret_cast<const float2 *>(fwin + idx + WW);
                 }
-#endif
             };
 #pragma unroll
             for (int s = 0; s < PF; ++s) issue(s);
@@ -1444,19 +1258,8 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 const float hh = 1.f - lh, hw = 1.f - lw;
                 const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
                 const float2 s01 = g01[s], s23 = g23[s];
-#if NLSPN_RES_EXP == 2  // timing experiment: gathers only, minimal arithmetic (wrong results)
-                (void)w1; (void)w2; (void)w3; (void)w4;
-                acc[e] += (s01.x + s01.y) + (s23.x + s23.y);
-#elif NLSPN_RES_FMA  // timing experiment: contracted bilinear (differs from the oracle)
-                float v = w1 * s01.x;
-                v = __builtin_fmaf(w2, s01.y, v);
-                v = __builtin_fmaf(w3, s23.x, v);
-                v = __builtin_fmaf(w4, s23.y, v);
-                acc[e] = __builtin_fmaf(v, av[e], acc[e]);
-#else
                 const float v = (w1 * s01.x + w2 * s01.y + w3 * s23.x + w4 * s23.y);
                 acc[e] += v * av[e];  // .cuh:189 col = val * mask, summed in tap order
-#endif
             }
             // general path (rare; only waves holding a tap outside the window): the
             // reference's per-corner checks, from global memory where needed (the same
@@ -1467,10 +1270,7 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 // the own quad's row and first column, recomputed from its byte offset (not
                 // live across the loop)
                 const int pe = (int)(vpix / ES), y = pe / W, x0 = pe - y * W;
-                if constexpr (TAIL) {  // (the quad's affinities are in VGPRs: re-read from global memory)
-#pragma unroll
-                    for (int e = 0; e < PX; ++e) acc[e] = gp_pixel(y, x0 + e, lown + e, vpix + e * ES, nullptr, 0);
-                } else {
+                {
                     // (the same sum written out, every loop rolled: the pixel, the tap and the
                     // corner; unrolled, this rare path's code cost the 128-thread build's loop
                     // 3 % of C1, profiles/r05/ab_gp_r5.txt)
@@ -1549,46 +1349,12 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             }
             // plane t + 1's poison acknowledged first (issued before the taps: no wait left)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (l2) PixVec<T, PX>::template store<0>(make_rsrc(p_out), vpix, 0u, o);  // kept in the XCD's L2
-            else PixVec<T, PX>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);   // write-through
+            if (ex) PixVec<T, PX>::template store<kSc1>(make_rsrc(p_out), vpix, 0u, o);  // write-through
+            else PixVec<T, PX>::template store<0>(make_rsrc(p_out), vpix, 0u, o);   // kept in the XCD's L2
 #pragma unroll
             for (int e = 0; e < PX; ++e) pown[e] = round_to<T>(o[e]);
             if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
                 PixVec<T, PX>::template store<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), vpix, 0u, fin);
-                }
-        // ---- TAIL: the tail pixel (waves 4..7, one per SIMD), the same arithmetic in the
-        // same order: taps 0..K-1 with the reference tap (one-cell form) at K/2
-        float pown_t = 0.f;
-        if (tail_wave && !(exp_dbg(a.dbg) & 4u)) {
-            if (tail_on) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) tail_tap(k);
-                float acc = tacc;
-                if (kResGeneralPath && has_fb_t && !(exp_dbg(a.dbg) & 64u)) {
-                    const int pe = (int)(tvpix / ES), gy = pe / W, gx = pe - gy * W;
-                    acc = gp_pixel(gy, gx, town, tvpix, tal, 256);
-                    gp_raise();
-                }
-                if (refull) {  // the four-corner reference tap (see the quad's form above)
-                    const float *r0p = &fwin[town], *r1p = r0p + WW;
-                    if (!__builtin_isfinite(r0p[1]) || !__builtin_isfinite(r1p[0]) || !__builtin_isfinite(r1p[1]))
-                        acc = __builtin_nanf("");
-                }
-                float vv = acc;
-                if (preserve) {
-                    const float dt = tal[256 * (K + 2)];
-                    const float m = dt > 0.f ? 1.f : 0.f;
-                    vv = (1.0f - m) * vv + m * dt;
-                }
-                if (clip) vv = clamp0(vv);
-                const float fin = clip ? vv : clamp0(vv);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its plane-(t+1) poison acknowledged
-                if (l2) ResVec<T>::template store1<0>(make_rsrc(p_out), tvpix, 0u, vv);
-                else ResVec<T>::template store1<kSc1>(make_rsrc(p_out), tvpix, 0u, vv);
-                pown_t = round_to<T>(vv);
-                if (t == a.T - 1 && !(exp_dbg(a.dbg) & 8u))
-                    ResVec<T>::template store1<0>(make_rsrc(static_cast<T *>(a.pred) + b * HW), tvpix, 0u, fin);
-            }
         }
         if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
         if (kResWTrace && trace && lane == 0) res_wtrace(a.pred, a.T, wbase, t)[0] = __builtin_amdgcn_s_memrealtime();
@@ -1610,16 +1376,10 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
             if (!__builtin_isfinite(fs))
                 ctl[6 + ((t + 1) & 1)] = 1;  // (benign race: every writer stores 1)
         }
-        if (tail_on && t < a.T - 1 && !(exp_dbg(a.dbg) & 2u)) {  // TAIL: the tail pixel's f_t
-            const float f = has_conf ? pown_t * tal[256 * (K + 1)] : pown_t;
-            fwin[town] = f;
-            fwinB[town - 1] = f;
-            if (!__builtin_isfinite(f)) ctl[6 + ((t + 1) & 1)] = 1;
-        }
         // fp16 storage with the prologue in the launch: iteration 1 used the normalisation's
         // own values (step 1 does); later iterations use them as stored, as the step launches
         // read them back (rounded to fp16, the reference-tap weight 1 - sum of the rounded ones)
-        if constexpr (!TAIL && ES == 2) {
+        if constexpr (ES == 2) {
             if (first && t == t0) {
                 float s4[PX], v[PX];
 #pragma unroll
@@ -1654,15 +1414,6 @@ __global__ void __launch_bounds__(MAXNT) prop_resident_kernel(ResArgs a) {
                 for (int tt = g2 == grp ? t_abort : t0; tt < a.T; ++tt)
                     PixVec<T, PX>::template store<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), vpix, 0u, qn);
                 PixVec<T, PX>::template store<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), vpix, 0u, qn);
-            }
-        }
-        if (tail_on) {
-            for (int g2 = grp; g2 < ngroups; ++g2) {
-                const int b2 = bl + g2 * a.B;
-                for (int tt = g2 == grp ? t_abort : t0; tt < a.T; ++tt)
-                    ResVec<T>::template store1<kSc1>(make_rsrc(p_out_all + (size_t)tt * a.tstride + b2 * HW), tvpix, 0u,
-                                                     __builtin_nanf(""));
-                ResVec<T>::template store1<kSc1>(make_rsrc(static_cast<T *>(a.pred) + b2 * HW), tvpix, 0u, __builtin_nanf(""));
             }
         }
         lds_barrier();  // (every wave of the part is here: the abort word is read after a barrier)

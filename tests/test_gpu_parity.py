@@ -178,19 +178,27 @@ def test_propagate_no_conf(oracle):
     dict(B=8, H=228, W=304, kernel=(3, 3), T=18),     # C2 (NYUv2, B=8) at full size
     dict(B=4, H=240, W=1216, kernel=(3, 3), T=18),    # C3 (KITTI-DC, B=4) at full size
 ])
-def test_full_size_vs_oracle(oracle, cfg):
+def test_full_size_vs_oracle(oracle, cfg, record_metric):
     K = cfg["kernel"][0] * cfg["kernel"][1] - 1
     s = synth(cfg["B"], cfg["H"], cfg["W"], K, seed=7240)
     o = gpu_propagate(s, gamma=0.5 * K, kernel=cfg["kernel"], T=cfg["T"])
     oracle.set_threads(16)
     e = oracle_propagate(oracle, s, gamma=0.5 * K, kernel=cfg["kernel"], T=cfg["T"])
-    assert rmse(host(o["pred"]), e["pred"]) < 1e-4
+    err = rmse(host(o["pred"]), e["pred"])
+    record_metric(f"full_{cfg['H']}x{cfg['W']}_b{cfg['B']}_rmse_pred", err)
+    assert err < 1e-4, err
+    # every output of the dict (nlspnmodel.py:375-381), as the C1 case checks it
+    np.testing.assert_allclose(host(o["pred_inter_tensor"]), e["pred_inter"], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(host(o["aff"]), e["aff"], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(host(o["offset"]), e["offset"])
+    np.testing.assert_array_equal(host(o["confidence"]), e["confidence"])
     p = host(o["pred"])
     assert p.min() >= 0 and p.max() <= 10.0  # convex operator: values stay in [0, max_depth]
 
 
-def test_fp16_vs_fp32_oracle(oracle):
-    """Config C5 in miniature: K=16 (1x17), T=36, fp16 storage vs fp32 oracle on fp16-rounded inputs."""
+def test_fp16_vs_fp32_oracle(oracle, record_metric):
+    """Config C5 in miniature: K=16 (1x17), T=36, fp16 storage vs fp32 oracle on fp16-rounded inputs.
+    Bars: a few times the measured RMSE (gpurun_out/metrics.jsonl), not BASELINE.md's 1e-2."""
     s = synth(2, 48, 64, 16, seed=5)
     for k in ("pred_init", "dep", "conf", "off_aff"):
         s[k] = s[k].astype(np.float16).astype(np.float32)
@@ -198,14 +206,20 @@ def test_fp16_vs_fp32_oracle(oracle):
     assert o["pred"].dtype == torch.float16
     e = oracle_propagate(oracle, s, gamma=8.0, kernel=(1, 17), T=36)
     err = rmse(host(o["pred"]), e["pred"])
-    assert err < 1e-2, err
+    err_inter = rmse(host(o["pred_inter_tensor"]), e["pred_inter"])
+    record_metric("c5_mini_fp16_rmse_pred", err)
+    record_metric("c5_mini_fp16_rmse_pred_inter", err_inter)
+    # measured (round 6): pred 1.13e-4, pred_inter 1.47e-4 — the denser default synth
+    assert err <= 3.5e-4, err
+    assert err_inter <= 5e-4, err_inter
 
 
 def test_c5_full_size_fp16_vs_fp32_oracle(oracle, record_metric):
     """Config C5 at full size (BASELINE.json configs[4]): NYU 228x304, B=16, K=16 (1x17),
     T=36, fp16 storage, against the fp32 oracle on the same fp16-rounded inputs.
-    Bar: RMSE <= 1e-2 on depth in [0, 10]; the measured value is
-    recorded (gpurun_out/metrics.jsonl)."""
+    BASELINE.md §5 allows RMSE <= 1e-2 on depth in [0, 10]; the bars here are ~3x the
+    measured values (round 5: pred 3.1e-5, pred_inter 1.08e-4), which are recorded
+    (gpurun_out/metrics.jsonl)."""
     s = synth(16, 228, 304, 16, seed=7240, density=500 / (228 * 304))
     for k in ("pred_init", "dep", "conf", "off_aff"):
         s[k] = s[k].astype(np.float16).astype(np.float32)
@@ -216,8 +230,8 @@ def test_c5_full_size_fp16_vs_fp32_oracle(oracle, record_metric):
     err_inter = rmse(host(o["pred_inter_tensor"]), e["pred_inter"])
     record_metric("c5_full_fp16_rmse_pred", err)
     record_metric("c5_full_fp16_rmse_pred_inter", err_inter)
-    assert err <= 1e-2, err
-    assert err_inter <= 1e-2, err_inter
+    assert err <= 1e-4, err
+    assert err_inter <= 5e-4, err_inter
     p = host(o["pred"])
     assert np.isfinite(p).all() and p.min() >= 0 and p.max() <= 10.0
 

@@ -66,18 +66,13 @@ def _both(inp, T=18, nan_ok=False, **kw):
     """(resident, steps): the default resident form (since round 5 the prologue and
     iteration 1 inside the resident launches, no step-1 launch), checked here against the
     resident form behind a step-1 launch (NLSPN_RES_FIRST=0), with every hand-off
-    write-through (NLSPN_RES_L2=0: no image's hand-offs kept in an XCD's L2), against the
-    other of the eight- and nine-wave builds where the eight-wave one applies
-    (NLSPN_RES_TAIL; the eight-wave build runs behind step 1), and the step form — every
-    pred_inter plane, pred and the prologue's output-dict tensors.
+    write-through (NLSPN_RES_L2=0: no line of any image kept in an XCD's L2), and the step
+    form — every pred_inter plane, pred and the prologue's output-dict tensors.
     nan_ok: NaN results compare by position (_nan_equal)."""
     with _env("1"):
         a = propagate(*inp, prop_time=T, **kw)
         with _env("0", "NLSPN_RES_L2"):
             c = propagate(*inp, prop_time=T, **kw)
-        # the other of the eight- and nine-wave builds where the eight-wave one applies
-        with _env("0" if _lib_tail_default() else "1", "NLSPN_RES_TAIL"):
-            d = propagate(*inp, prop_time=T, **kw)
         with _env("0", "NLSPN_RES_FIRST"):
             f = propagate(*inp, prop_time=T, **kw)
         with _env("0", "NLSPN_RES_SPLIT"):  # (small parts: one thread per quad instead of four)
@@ -91,13 +86,10 @@ def _both(inp, T=18, nan_ok=False, **kw):
         if a[k] is not None or b[k] is not None:
             assert _bits_equal(a[k], b[k]), k
             assert _bits_equal(c[k], b[k]), k
-            assert _bits_equal(d[k], b[k]), k
             assert _bits_equal(f[k], b[k]), k
     eq = _nan_equal if nan_ok else _bits_equal
     assert eq(a["pred_inter_tensor"], c["pred_inter_tensor"]), "resident forms differ"
     assert eq(a["pred"], c["pred"])
-    assert eq(a["pred_inter_tensor"], d["pred_inter_tensor"]), "eight-wave and nine-wave builds differ"
-    assert eq(a["pred"], d["pred"])
     assert eq(a["pred_inter_tensor"], f["pred_inter_tensor"]), "prologue in the launch and step 1 differ"
     assert eq(a["pred"], f["pred"])
     assert eq(a["pred_inter_tensor"], g["pred_inter_tensor"]), "split-quad and quad-per-thread builds differ"
@@ -105,16 +97,6 @@ def _both(inp, T=18, nan_ok=False, **kw):
     assert eq(a["pred_inter_tensor"], h["pred_inter_tensor"]), "four- and two-thread split-quad builds differ"
     assert eq(a["pred"], h["pred"])
     return a, b
-
-
-def _lib_tail_default():
-    """Whether the library plans the eight-wave build by default at the C2 shape."""
-    old = os.environ.pop("NLSPN_RES_TAIL", None)
-    try:
-        return resident_config(8, 228, 304)[2] == 512
-    finally:
-        if old is not None:
-            os.environ["NLSPN_RES_TAIL"] = old
 
 
 def _bits_equal(x, y):
@@ -126,17 +108,10 @@ def _bits_equal(x, y):
 def test_resident_engaged_at_c2():
     with _env("1"):
         ok, grid, block, lds = resident_config(8, 228, 304)
-        assert ok and grid == 256 and block in (512, 576) and lds > 80 * 1024
-        ok, grid, block, lds = resident_config(4, 240, 1216)  # C3: two launches of 2 images x 128 parts
-        assert ok and grid == 256 and block in (512, 576) and lds > 80 * 1024
-        # C2 / C3 shapes: the nine-wave build, or the eight-wave one (512 threads, quads + tail
-        # pixels; fp32)
-        with _env("1", "NLSPN_RES_TAIL"):
-            assert resident_config(8, 228, 304)[2] == 512
-            assert resident_config(4, 240, 1216)[2] == 512
-            assert resident_config(8, 228, 304, dtype=1)[2] == 576  # fp16: the nine-wave build
-        with _env("0", "NLSPN_RES_TAIL"):
-            assert resident_config(8, 228, 304)[2] == 576
+        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
+        ok, grid, block, lds = resident_config(4, 240, 1216)  # C3: two groups of 2 images x 128 parts
+        assert ok and grid == 256 and block == 576 and lds > 80 * 1024
+        assert resident_config(8, 228, 304, dtype=1)[2] == 576  # fp16
         assert not resident_config(8, 228, 302)[0]       # W % 4 != 0
         ok, grid, block, lds = resident_config(1, 228, 304)  # C1: one image in 13 x 19 parts of 72 quads,
         assert ok and grid == 247 and block == 320          # four threads per quad (a split-quad build)
@@ -155,7 +130,7 @@ def test_resident_engaged_at_c2():
     (8, 228, 304, 2.0, torch.float32, True, {"always_clip": True}),
     (8, 228, 304, 2.0, torch.float32, False, {"preserve_input": False}),
     (8, 228, 304, 2.0, torch.float16, True, {}),                        # fp16 storage
-    (8, 228, 304, 12.0, torch.float32, True, {"always_clip": True}),    # C2 parts, fixed halo: tail pixels' general path
+    (8, 228, 304, 12.0, torch.float32, True, {"always_clip": True}),    # C2 parts, fixed halo: the general path
     (4, 96, 128, 12.0, torch.float32, True, {}),                        # taps beyond the halo
     (2, 64, 96, 60.0, torch.float32, True, {"affinity": "TC"}),         # mostly out of image, long ranges
     (1, 24, 32, 2.0, torch.float32, True, {}),                          # 3 tiny parts
@@ -307,27 +282,33 @@ def test_resident_replays_stable_and_no_abort():
         plan.close()
 
 
-@pytest.mark.parametrize("B,H,W,l2,dtype,sigma", [
-    (8, 228, 304, "1", torch.float32, 3.0), (8, 228, 304, "0", torch.float32, 3.0),
-    (4, 240, 1216, "1", torch.float32, 3.0), (1, 228, 304, "1", torch.float32, 3.0),
-    (8, 228, 304, "1", torch.float16, 3.0),
-    (8, 228, 304, "1", torch.float32, 12.0), (2, 120, 2048, "1", torch.float32, 12.0)])
-def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype, sigma):
+@pytest.mark.parametrize("B,H,W,l2,dtype,sigma,kernel,T", [
+    (8, 228, 304, "1", torch.float32, 3.0, (3, 3), 18), (8, 228, 304, "0", torch.float32, 3.0, (3, 3), 18),
+    (4, 240, 1216, "1", torch.float32, 3.0, (3, 3), 18), (1, 228, 304, "1", torch.float32, 3.0, (3, 3), 18),
+    (8, 228, 304, "1", torch.float16, 3.0, (3, 3), 18),
+    (4, 240, 1216, "1", torch.float16, 3.0, (3, 3), 18),                 # C3 shape, fp16 lines (16 quads)
+    (16, 228, 304, "1", torch.float16, 3.0, (1, 17), 36),                # C5: four groups, images over two XCDs
+    (16, 228, 304, "0", torch.float16, 3.0, (1, 17), 36),
+    (8, 228, 304, "1", torch.float32, 12.0, (3, 3), 18), (2, 120, 2048, "1", torch.float32, 12.0, (3, 3), 18)])
+def test_resident_alternating_inputs_no_stale_reads(B, H, W, l2, dtype, sigma, kernel, T):
     """Replays over in-place refilled inputs that alternate between two data sets: every
     plane a hand-off reads was last written with the OTHER set's values, so a consumer that
     took a previous call's cell instead of waiting out the poison (nlspn_resident.h) changes
-    the result.  Long-range offsets (sigma 3), L2-kept and write-through hand-offs, the
-    two-group merged launch (KITTI B=4), one image over 247 parts, fp16 storage; and two
-    fixed-halo shapes at sigma 12 whose far taps take the general path (global re-reads of
-    the same cells every iteration; test_general_path_taken_at_fixed_halo_shapes)."""
-    ia, _ = _inputs(B, H, W, sigma=sigma, seed=31, dtype=dtype)
-    ib, _ = _inputs(B, H, W, sigma=sigma, seed=32, dtype=dtype)
+    the result.  Long-range offsets (sigma 3), per-line hand-offs (lines no part on another
+    XCC reads kept in L2, the rest write-through) and every line write-through (l2 "0"), the
+    two-group merged launch (KITTI B=4), one image over 247 parts, fp16 storage, C5's four
+    image groups of 1x17 taps; and two fixed-halo shapes at sigma 12 whose far taps take the
+    general path (global re-reads of the same cells every iteration, whole-image published
+    windows; test_general_path_taken_at_fixed_halo_shapes)."""
+    K = kernel[0] * kernel[1] - 1
+    ia, _ = _inputs(B, H, W, sigma=sigma, seed=31, dtype=dtype, K=K)
+    ib, _ = _inputs(B, H, W, sigma=sigma, seed=32, dtype=dtype, K=K)
     with _env("0"):
-        ra = propagate(*ia, prop_time=18)["pred_inter_tensor"].clone()
-        rb = propagate(*ib, prop_time=18)["pred_inter_tensor"].clone()
+        ra = propagate(*ia, prop_time=T, kernel=kernel)["pred_inter_tensor"].clone()
+        rb = propagate(*ib, prop_time=T, kernel=kernel)["pred_inter_tensor"].clone()
     buf = [None if x is None else x.clone() for x in ia]
     with _env("1"), _env(l2, "NLSPN_RES_L2"):
-        plan = PropagationPlan(*buf, prop_time=18)
+        plan = PropagationPlan(*buf, prop_time=T, kernel=kernel)
         for i in range(12):
             src, ref = (ia, ra) if i % 2 == 0 else (ib, rb)
             for d, x in zip(buf, src):
