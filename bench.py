@@ -360,29 +360,38 @@ def gru_section_timing(inputs, cfg, steps, dev):
     off_aff = torch.cat([inputs["off"], inputs["aff"]], 1).contiguous()
     heads = (inputs["pred_init"], off_aff, inputs["conf"], inputs["dep"])
     assert off_aff.shape[1] == 3 * K
-    g = SectionGraph(m, *heads)
     e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    with torch.no_grad():
-        for _ in range(3):
-            m.propagate_heads(*heads)
-            g.replay()
+
+    def timed(native):
+        m.native_gru = native
+        g = SectionGraph(m, *heads)
+        with torch.no_grad():
+            for _ in range(3):
+                m.propagate_heads(*heads)
+                g.replay()
+            torch.cuda.synchronize()
+            e[0].record()
+            for _ in range(steps):
+                m.propagate_heads(*heads)
+            e[1].record()
+            e[2].record()
+            for _ in range(steps):
+                g.replay()
+            e[3].record()
         torch.cuda.synchronize()
-        e[0].record()
-        for _ in range(steps):
-            m.propagate_heads(*heads)
-        e[1].record()
-        e[2].record()
-        for _ in range(steps):
-            g.replay()
-        e[3].record()
-    torch.cuda.synchronize()
-    eager, graph = e[0].elapsed_time(e[1]) / steps, e[2].elapsed_time(e[3]) / steps
-    del g
-    # the same section with the GRU convolutions in channels_last and MIOpen's algorithm
-    # search on (NLSPNModel.gru_channels_last; cudnn.benchmark restored afterwards)
+        del g
+        return e[0].elapsed_time(e[1]) / steps, e[2].elapsed_time(e[3]) / steps
+
+    # the GRU-mode convolutions on the HIP kernels (gru.py, the model's inference default) ...
+    eager, graph = timed(True)
+    # ... and on the torch modules (MIOpen), NCHW with MIOpen's default algorithms
+    m_eager, m_graph = timed(False)
+    # the modules with the GRU convolutions in channels_last and MIOpen's algorithm search on
+    # (NLSPNModel.gru_channels_last; cudnn.benchmark restored afterwards)
     prev = torch.backends.cudnn.benchmark
     torch.backends.cudnn.benchmark = True
     try:
+        m.native_gru = False
         m.gru_channels_last()
         g = SectionGraph(m, *heads)
         with torch.no_grad():
@@ -399,9 +408,13 @@ def gru_section_timing(inputs, cfg, steps, dev):
         torch.backends.cudnn.benchmark = prev
     return {"ms_per_step_eager": round(eager, 4), "ms_per_step_graph": round(graph, 4),
             "iters_per_s_graph": round(cfg["T"] / (graph * 1e-3), 1),
-            "ms_per_step_graph_channels_last_tuned": round(tuned, 4), "steps": steps,
-            "note": "ConvGRU (MIOpen convs, hidden 128) + affinity normalisation + prop_step per iteration; "
-                    "tuned = GRU convs channels_last + MIOpen algorithm search"}
+            "modules": {"ms_per_step_eager": round(m_eager, 4), "ms_per_step_graph": round(m_graph, 4),
+                        "ms_per_step_graph_channels_last_tuned": round(tuned, 4)},
+            "speedup_vs_tuned_modules": round(tuned / graph, 3), "steps": steps,
+            "note": "per iteration: encode_dep, ConvGRU (hidden 128), decode_aff + crop as HIP f32-MFMA convolutions "
+                    "(gru.py; the first update also encode_aff), affinity normalisation, prop_step; graph = one "
+                    "hipGraph replay of the section (SectionGraph). modules: the same section on the torch modules "
+                    "(MIOpen), default and channels_last + MIOpen algorithm search"}
 
 
 def head_epilogue_timing(cfg, dev, reps=20):

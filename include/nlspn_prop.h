@@ -384,6 +384,42 @@ int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T,
  */
 int nlspn_resident_status(int clear);
 
+/*
+ * GRU-mode convolutions (the reference's forced default mode, src/config.py:225-228): one
+ * convolution of a GRU-mode iteration, f32 NCHW, inference (nlspnmodel.py:365-373), on the
+ * f32-input matrix cores with bias and activation in the epilogue (csrc/nlspn_gconv.h).
+ * Replaces the torch/MIOpen module calls of
+ *   encode_dep / encode_aff   (:127-138)  NLSPN_GC_S2 / NLSPN_GC_S2_C16: 3x3 stride 2 pad 1
+ *   ConvGRU                   (:386-403)  NLSPN_GC_GRU1 then NLSPN_GC_GRU2
+ *   decode_aff + _clip_as     (:140-143, :228-250)  NLSPN_GC_T2 / NLSPN_GC_T2_C16: 3x3
+ *                                          transposed stride 2 pad 1 output pad 1
+ * x0 (c0 channels) then x1 (c1 channels, may be null with c1 = 0) are the input channels
+ * (torch.cat order, read in place); Hi x Wi the input size.  wpk: the weights packed by
+ * nlspn_gconv_pack_layout's layout (nlspn_eccv20_amd/gru.py packs them), bias padded to
+ * the co tiles.  NLSPN_GC_S2* / NLSPN_GC_T2*: y = act(conv + bias) stored as (B, cout, ohs,
+ * ows) (ohs / ows <= the full output size: the crop), act NLSPN_GC_ACT_*, inputs divided by
+ * in_div while read (encode_dep's new_pred / max_depth; 1: none).  NLSPN_GC_GRU1 (x0 = h, x1
+ * = x, cout = 3 hc): z, r*h and qx (convq's x half + bias) into zb / rhb / qxb;
+ * NLSPN_GC_GRU2 (x0 = rhb, c1 = 0, cout = hc): h' = (1 - z) h + z tanh(convq's r*h half +
+ * qx) into hout.  Returns NLSPN_EUNSUPPORTED when a shape's window does not fit the kernel.
+ */
+#define NLSPN_GC_S2 0
+#define NLSPN_GC_S2_C16 1
+#define NLSPN_GC_GRU1 2
+#define NLSPN_GC_GRU2 3
+#define NLSPN_GC_T2 4
+#define NLSPN_GC_T2_C16 5
+#define NLSPN_GC_ACT_NONE 0
+#define NLSPN_GC_ACT_RELU 1
+#define NLSPN_GC_ACT_TANH 2
+/* the packed weight layout of a preset: *co_tile output channels per tile, *cin_chunk input
+ * channels per chunk (the packed input channel count is a multiple), *transposed */
+int nlspn_gconv_pack_layout(int layer, int *co_tile, int *cin_chunk, int *transposed);
+int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk,
+                const float *bias, float *y, const float *h, float *zb, float *rhb, float *qxb,
+                float *hout, int B, int Hi, int Wi, int cout, int ohs, int ows, int act,
+                float in_div, int hc, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

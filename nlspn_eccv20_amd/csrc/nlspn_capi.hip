@@ -21,6 +21,7 @@
 #include "nlspn_resident.h"
 #include "nlspn_s2d.h"
 #include "nlspn_heads.h"
+#include "nlspn_gconv.h"
 
 // defined in nlspn_kern_resident.hip (3x3) and nlspn_kern_resident_wide.hip (1x17, 5x5)
 // (own translation units and flags)
@@ -65,6 +66,9 @@ extern template __global__ void heads_kernel<1, true, 2>(HeadsArgs);
 extern template __global__ void heads_kernel<1, true, 3>(HeadsArgs);
 extern template __global__ void heads_kernel<1, true, 0, true>(HeadsArgs);
 extern template __global__ void heads_kernel<1, false, 0, true>(HeadsArgs);
+// defined in nlspn_kern_gconv.hip
+#define NLSPN_GC_EXTERN(id, ...) extern template __global__ void gconv_kernel<__VA_ARGS__>(GconvArgs);
+NLSPN_GC_CONFIGS(NLSPN_GC_EXTERN)
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -1585,6 +1589,100 @@ int nlspn_resident_status(int clear) {
              "a resident propagation launch on this device aborted (a part waited past its spin limit: the grid "
              "was not co-resident); its outputs were filled with NaN");
     return v ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- GRU-mode convolutions
+}  // extern "C"
+namespace {
+struct GcPreset {
+    const void *fn;
+    int mode, wgco, npx, xr, xp, lds, epi;
+};
+template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI>
+GcPreset gc_preset() {
+    using Cfg = GcCfg<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI>;
+    return GcPreset{reinterpret_cast<const void *>(&gconv_kernel<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI>), MODE,
+                    Cfg::WGCO, Cfg::NPX, XR, XP, (int)(Cfg::LDS_FLOATS * sizeof(float)), EPI};
+}
+bool gc_get(int layer, GcPreset &p) {
+    switch (layer) {
+#define NLSPN_GC_CASE(id, ...) \
+    case id: p = gc_preset<__VA_ARGS__>(); return true;
+        NLSPN_GC_CONFIGS(NLSPN_GC_CASE)
+        default: return false;
+    }
+}
+}  // namespace
+extern "C" {
+
+int nlspn_gconv_pack_layout(int layer, int *co_tile, int *cin_chunk, int *transposed) {
+    GcPreset p;
+    if (!gc_get(layer, p)) return fail(NLSPN_EINVAL, "unknown GRU-mode conv preset %d", layer);
+    if (co_tile) *co_tile = p.wgco;
+    if (cin_chunk) *cin_chunk = kGcCP;
+    if (transposed) *transposed = p.mode == kGcT2;
+    return NLSPN_OK;
+}
+
+int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk, const float *bias,
+                float *y, const float *h, float *zb, float *rhb, float *qxb, float *hout, int B, int Hi, int Wi,
+                int cout, int ohs, int ows, int act, float in_div, int hc, void *stream) {
+    GcPreset p;
+    if (!gc_get(layer, p)) return fail(NLSPN_EINVAL, "unknown GRU-mode conv preset %d", layer);
+    if (B < 1 || Hi < 1 || Wi < 1 || cout < 1 || c0 < 1 || c1 < 0 || (c1 > 0 && !x1))
+        return fail(NLSPN_EINVAL, "gconv: bad shape B=%d Hi=%d Wi=%d c0=%d c1=%d cout=%d", B, Hi, Wi, c0, c1, cout);
+    if (!x0 || !wpk || !bias) return fail(NLSPN_EINVAL, "gconv: null input, weights or bias");
+    const bool gru = p.epi != kGcEpiAct, gru1 = p.epi == kGcEpiGru1;
+    GconvArgs a{};
+    a.x0 = x0; a.x1 = x1; a.w = wpk; a.bias = bias; a.y = y;
+    a.h = h; a.zb = zb; a.rhb = rhb; a.qxb = qxb; a.hout = hout;
+    a.c0 = c0; a.c1 = c1; a.cin_pad = (c0 + c1 + kGcCP - 1) / kGcCP * kGcCP;
+    a.B = B; a.Hi = Hi; a.Wi = Wi;
+    if (p.mode == kGcS1) { a.Ho = Hi; a.Wo = Wi; }
+    else if (p.mode == kGcS2) { a.Ho = (Hi - 1) / 2 + 1; a.Wo = (Wi - 1) / 2 + 1; }
+    else { a.Ho = 2 * Hi; a.Wo = 2 * Wi; }
+    a.ohs = gru ? a.Ho : ohs;
+    a.ows = gru ? a.Wo : ows;
+    if (a.ohs < 1 || a.ows < 1 || a.ohs > a.Ho || a.ows > a.Wo)
+        return fail(NLSPN_EINVAL, "gconv: stored size %dx%d outside the output %dx%d", a.ohs, a.ows, a.Ho, a.Wo);
+    a.cout = cout;
+    a.co_tiles = (cout + p.wgco - 1) / p.wgco;
+    a.act = act;
+    a.in_div = in_div;
+    a.hc = hc;
+    if (gru) {
+        if (hc < 1 || hc % p.wgco != 0 || !h || (gru1 ? (!zb || !rhb || !qxb || cout != 3 * hc || c0 != hc)
+                                                                          : (!zb || !qxb || !hout || cout != hc || c1 != 0 || c0 != hc)))
+            return fail(NLSPN_EINVAL, "gconv: GRU launch needs hc %% %d == 0, h, z / r*h / qx buffers and cout 3hc (GRU1) "
+                        "or hc (GRU2)", p.wgco);
+    } else if (!y) {
+        return fail(NLSPN_EINVAL, "gconv: null output");
+    }
+    a.gh = p.mode == kGcT2 ? Hi : a.Ho;
+    a.gw = p.mode == kGcT2 ? Wi : a.Wo;
+    // column bands: the window's columns within the LDS pitch
+    const int bwmax = p.mode == kGcS1 ? p.xp - 2 : p.mode == kGcS2 ? (p.xp - 3) / 2 + 1 : p.xp - 1;
+    a.nbands = (a.gw + bwmax - 1) / bwmax;
+    a.bw = (a.gw + a.nbands - 1) / a.nbands;
+    // the rows a tile of npx pixels spans (at most (npx + bw - 2) / bw row steps), within the
+    // window's XR rows: narrow bands take fewer pixels per tile
+    const auto rows_of = [&](int npx) {
+        const int dr = (npx + a.bw - 2) / a.bw;
+        return p.mode == kGcS1 ? dr + 3 : p.mode == kGcS2 ? 2 * dr + 3 : dr + 2;
+    };
+    a.npx = p.npx;
+    while (a.npx > 1 && rows_of(a.npx) > p.xr) --a.npx;
+    if (rows_of(a.npx) > p.xr)
+        return fail(NLSPN_EUNSUPPORTED, "gconv: a tile of a %d-wide band spans more than %d window rows", a.bw, p.xr);
+    a.tpb = (a.gh * a.bw + a.npx - 1) / a.npx;
+    const long long nwg = (long long)(p.mode == kGcT2 ? 4 : 1) * a.co_tiles * B * a.nbands * a.tpb;
+    // (one image's channels of a source within a 32-bit buffer descriptor)
+    if (nwg > 0x7fffffffLL || (long long)std::max(c0, c1) * Hi * Wi * 4 > 0x7fffffffLL)
+        return fail(NLSPN_EINVAL, "gconv: problem too large");
+    if (int rc = set_lds_attr(p.fn, p.lds)) return rc;
+    void *args[] = {&a};
+    NLSPN_HIP_TRY(hipLaunchKernel(p.fn, dim3((unsigned)nwg), dim3(kGcNT), args, (size_t)p.lds, as_stream(stream)));
+    return check_launch("nlspn_gconv");
 }
 
 int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf, int *grid,

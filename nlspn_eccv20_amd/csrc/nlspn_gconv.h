@@ -1,0 +1,395 @@
+// GRU-mode convolutions (the reference's forced default, src/config.py:225-228):
+// every convolution of one GRU-mode iteration (nlspnmodel.py:365-373) —
+//   dep_feat = encode_dep(new_pred / max_depth)   3x3 stride-2 convs + bias + ReLU   (:134-138)
+//   aff_feat = encode_aff(aff)  (first update)    3x3 stride-2 convs + bias, ReLU / Tanh (:127-132)
+//   aff_feat = GRU(h=aff_feat, x=dep_feat)        ConvGRU, three 3x3 convs         (:386-403)
+//   aff      = decode_aff(aff_feat)               3x3 stride-2 transposed convs    (:140-143)
+//                                                 + the _clip_as crop (:237-250)
+// as implicit GEMMs on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: f32 operands,
+// exact f32 products, f32 accumulation; only the summation order differs from a
+// sequential f32 convolution), NCHW in and out, with bias and activation in the epilogue —
+// no torch.cat, no layout conversions, no separate bias / ReLU / sigmoid / tanh kernels.
+//
+// The ConvGRU as two launches (the candidate needs r at the neighbouring pixels):
+//   GRU1: output channels 0..127 z = sigmoid(convz(cat(h, x))), 128..255 r = sigmoid(convr(..))
+//         stored as r*h, 256..383 qx = convq's x half + bias (its K runs over x only);
+//   GRU2: q = tanh(convq's r*h half + qx); h' = (1 - z) h + z q.
+//
+// GEMM: D[co][px] = sum_k W[co][k] X[k][px], k = (input channel, tap).  A workgroup of 4
+// waves (WGM x WGN) owns 16*WM*WGM output channels x 16*WN*WGN pixels; a wave owns WM x WN
+// 16x16 blocks (lane l: A[co = l & 15][k = l >> 4], B[k = l >> 4][px = l & 15], so a k-step
+// is 4 input channels at one tap).  Pixels: the output grid (a transposed conv: one output
+// phase's grid, = the input grid) is cut into column bands of width bw, and a band into flat
+// row-major runs of NPX pixels — no tile columns wasted on a 38-pixel-wide 1/8-scale image.
+// Per chunk of CC input channels the workgroup stages the packed weights [ci][tap][co] and
+// the input window (the rows / columns its pixels' taps reach, zero outside the image = the
+// zero padding) in LDS; the next chunk's global loads are in flight in registers while the
+// current chunk computes.  The LDS window pitch XP is a compile-time constant, so every
+// operand read is one ds_read_b32 with an immediate offset from a per-lane base.
+#pragma once
+
+#include "nlspn_common.h"
+
+namespace nlspn {
+
+constexpr int kGcNT = 256;  // threads per workgroup (4 waves)
+constexpr int kGcCP = 16;   // packed input channels: a multiple of this (every chunk size CC divides it)
+enum { kGcS1 = 0, kGcS2 = 1, kGcT2 = 2 };         // 3x3 pad 1 stride 1 / stride 2; transposed stride 2 (pad 1, output pad 1)
+enum { kGcEpiAct = 0, kGcEpiGru1 = 1, kGcEpiGru2 = 2 };
+enum { kGcActNone = 0, kGcActRelu = 1, kGcActTanh = 2 };
+
+struct GconvArgs {
+    const float *x0, *x1;  // inputs (B, c0, Hi, Wi) and (B, c1, Hi, Wi): channels [0, c0) and [c0, c0 + c1)
+    const float *w;        // packed weights [phase][co_tile][cin_pad][ntap][WGco] (phase: transposed only)
+    const float *bias;     // [co_tiles * WGco] (zero past cout)
+    float *y;              // kGcEpiAct: (B, cout, ohs, ows)
+    // ConvGRU (kGcEpiGru*): h the hidden state (B, hc, Ho, Wo); z, r*h and qx of GRU1
+    const float *h;
+    float *zb, *rhb, *qxb;
+    float *hout;           // GRU2: h'
+    int c0, c1, cin_pad;   // cin_pad = roundup(c0 + c1, kGcCP)
+    int B, Hi, Wi, Ho, Wo;
+    int ohs, ows;          // stored rows / columns of y (the crop: rows >= ohs / columns >= ows are not stored)
+    int cout, co_tiles;
+    int gh, gw;            // the pixel grid tiled (convolutions: Ho x Wo; transposed: Hi x Wi per phase)
+    int bw, nbands, tpb;   // band width, bands, tiles per band (of the widest band)
+    int npx;               // pixels per tile (<= NPX: a narrow band's tile must fit the window rows)
+    int act;               // kGcAct*
+    float in_div;          // inputs divided by it while staged (encode_dep: max_depth, :366); 1: as they are
+    int hc;                // GRU hidden channels
+};
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// taps of a transposed stride-2 pad-1 3x3 conv landing on output phase (py, px): kernel row ky
+// reaches output row oy = 2 iy - 1 + ky, so oy = 2 qy + py takes ky = 1 (py = 0, iy = qy) or
+// ky = 0 / 2 (py = 1, iy = qy + 1 / qy)
+__host__ __device__ constexpr int gc_ntap(int mode, int phase) {
+    return mode != kGcT2 ? 9 : ((phase >> 1) ? 2 : 1) * ((phase & 1) ? 2 : 1);
+}
+// the tap's kernel row / column (ky, kx) and its window offset (dy, dx) for tap index t
+template <int MODE, int PH>
+__device__ __forceinline__ constexpr void gc_tap(int t, int &ky, int &kx, int &dy, int &dx) {
+    if constexpr (MODE != kGcT2) {
+        ky = t / 3; kx = t % 3; dy = ky; dx = kx;
+    } else {
+        constexpr int py = PH >> 1, px = PH & 1, nx = px ? 2 : 1;
+        const int ty = t / nx, tx = t % nx;
+        ky = py ? 2 * ty : 1;   // py = 1: ky 0 then 2
+        kx = px ? 2 * tx : 1;
+        dy = (py + 1 - ky) / 2;  // window row offset (iy - qy)
+        dx = (px + 1 - kx) / 2;
+    }
+}
+
+template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI>
+struct GcCfg {
+    static constexpr int WGCO = 16 * WM * WGM, NPX = 16 * WN * WGN;
+    static constexpr int NTMAX = MODE == kGcT2 ? 4 : 9;
+    // LDS: weights [CC][NTMAX][WGCO] (+16 floats per channel: the four lane groups' rows start
+    // 16 banks apart), input window [CC][XR][XP] (+16 per channel)
+    static constexpr int WCS = NTMAX * WGCO + 16;
+    static constexpr int XCS = XR * XP + 16;
+    static constexpr int LDS_FLOATS = CC * WCS + CC * XCS;
+    static constexpr int WREG = (CC * NTMAX * WGCO + kGcNT - 1) / kGcNT;   // prefetch registers (weights)
+    static constexpr int XREG = (CC * XR * XP + kGcNT - 1) / kGcNT;     // prefetch registers (window)
+};
+
+template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI, int PH>
+__device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int wgi) {
+    using Cfg = GcCfg<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI>;
+    constexpr int WGCO = Cfg::WGCO, NPX = Cfg::NPX, WCS = Cfg::WCS, XCS = Cfg::XCS;
+    constexpr int NTAP = gc_ntap(MODE, PH);
+    constexpr int S = MODE == kGcS2 ? 2 : 1;
+    float *Ws = lds;
+    float *Xs = lds + CC * WCS;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv % WGM, wn = wv / WGM;
+    const int l16 = lane & 15, lg = lane >> 4;
+
+    // workgroup -> (co tile, image, band, tile); the phase is PH
+    const int cot = wgi % a.co_tiles;
+    int rest = wgi / a.co_tiles;
+    const int tile = rest % a.tpb;
+    rest /= a.tpb;
+    const int band = rest % a.nbands;
+    const int b = rest / a.nbands;
+    const int bx0 = band * a.bw, bwi = min(a.bw, a.gw - bx0);
+    const int npx = a.npx;
+    const int f0 = tile * npx;
+    if (f0 >= a.gh * bwi) return;  // (the narrower last band has fewer tiles)
+    const int ra = f0 / bwi, rb = min(a.gh - 1, (f0 + npx - 1) / bwi);
+    // the window: input rows iy0 .. iy0 + nrows - 1, columns ix0 .. ix0 + ncols - 1
+    const int iy0 = MODE == kGcT2 ? ra : S * ra - 1;
+    const int ix0 = MODE == kGcT2 ? bx0 : S * bx0 - 1;
+    const int nrows = MODE == kGcT2 ? rb - ra + 2 : S * (rb - ra) + 3;
+    const int ncols = MODE == kGcT2 ? bwi + 1 : S * (bwi - 1) + 3;
+
+    // per n-block: this lane's pixel (grid row gy, column gx) and its window base
+    int gyv[WN], gxv[WN], xb[WN];
+#pragma unroll
+    for (int n = 0; n < WN; ++n) {
+        const int jj = 16 * (wn * WN + n) + l16;
+        const int f = f0 + min(jj, npx - 1);
+        const int gy = f / bwi, gx = bx0 + (f - gy * bwi);
+        gyv[n] = jj < npx ? gy : a.gh;  // (past the tile: not stored)
+        gxv[n] = gx;
+        // (a pixel past the grid reads a clamped in-window cell; its result is not stored)
+        const int ry = min(gy, rb) - ra;
+        xb[n] = lg * XCS + (S * ry) * XP + S * (gx - bx0);
+    }
+    const int wb = lg * WCS + wm * (16 * WM) + l16;
+
+    // the K range: GRU1's qx tile (co 2hc .. 3hc - 1) runs over x's channels only
+    int cs = 0;
+    if constexpr (EPI == kGcEpiGru1) cs = (cot * WGCO >= 2 * a.hc) ? a.c0 : 0;
+    // (chunks up to the last input channel: the packing pads the channels to kGcCP, a chunk of
+    // CC < kGcCP channels past the last one is skipped, not read)
+    const int ce = min(a.cin_pad, (a.c0 + a.c1 + CC - 1) / CC * CC);
+    const long long HWi = (long long)a.Hi * a.Wi;
+    // (transposed: the phases' taps are packed one after another, 1 + 2 + 2 + 4 = 9)
+    constexpr int TAP0 = MODE == kGcT2 ? (PH == 0 ? 0 : PH == 1 ? 1 : PH == 2 ? 3 : 5) : 0;
+    const float *wsrc = a.w + (long long)a.cin_pad * WGCO * ((long long)TAP0 * a.co_tiles + (long long)cot * NTAP);
+
+    // Staging.  The window cells a thread loads are the same every chunk, only the channels
+    // change: each cell's byte offset within a chunk's channels is computed once (0x80000000
+    // for a cell outside the window or the image: the buffer load returns 0 = the zero
+    // padding), and a chunk is one buffer descriptor whose size ends at the source's last
+    // channel (channels past it, the chunk's padding, read 0 too).  The weights of a chunk
+    // are contiguous: 16-byte loads.
+    constexpr int WF4 = CC * NTAP * WGCO / 4;  // float4s of a chunk's weights
+    constexpr int WR4 = (WF4 + kGcNT - 1) / kGcNT;
+    unsigned xoff[Cfg::XREG];
+#pragma unroll
+    for (int i = 0; i < Cfg::XREG; ++i) {
+        const int e = tid + i * kGcNT;
+        const int c = e / (XR * XP), rem = e - c * (XR * XP);
+        const int row = rem / XP, col = rem - row * XP;
+        const int iy = iy0 + row, ix = ix0 + col;
+        const bool ok = c < CC && row < nrows && col < ncols && (unsigned)iy < (unsigned)a.Hi &&
+                        (unsigned)ix < (unsigned)a.Wi;
+        xoff[i] = ok ? (unsigned)(((long long)c * HWi + (long long)iy * a.Wi + ix) * 4) : 0x80000000u;
+    }
+    // two register sets: chunk k + 2's loads are issued while chunk k computes, so a load has
+    // two chunks' MFMAs to land (one chunk's, at one wave per SIMD, left L2 latency exposed)
+    struct Regs {
+        f32x4 wr[WR4];
+        float xr[Cfg::XREG];
+    };
+    auto load_chunk = [&](int c0, Regs &R) __attribute__((always_inline)) {
+        const rsrc_t rw = make_rsrc(wsrc + (long long)c0 * NTAP * WGCO);
+#pragma unroll
+        for (int i = 0; i < WR4; ++i) {
+            const int e = min(tid + i * kGcNT, WF4 - 1);
+            R.wr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)e * 16u, 0u, 0));
+        }
+        // (a chunk past the last channel — possible only within the 16-channel packing pad, which
+        // the loop bound below excludes — would read nothing: an empty descriptor on x0)
+        const bool s0 = c0 < a.c0;
+        const int nch = s0 ? a.c0 - c0 : a.c1 - (c0 - a.c0);
+        const bool any = nch > 0 && (s0 || a.x1 != nullptr);
+        const float *base = !any ? a.x0
+                            : s0 ? a.x0 + ((long long)b * a.c0 + c0) * HWi
+                                 : a.x1 + ((long long)b * a.c1 + (c0 - a.c0)) * HWi;
+        const int nrec = any ? (int)(nch * HWi * 4) : 0;
+        const rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < Cfg::XREG; ++i)
+            R.xr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, xoff[i], 0u, 0));
+    };
+    auto store_chunk = [&](const Regs &R) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < WR4; ++i) {
+            const int e = tid + i * kGcNT;
+            if (e < WF4) {
+                const int c = (4 * e) / (NTAP * WGCO), rem = 4 * e - c * (NTAP * WGCO);
+                *reinterpret_cast<f32x4 *>(&Ws[c * WCS + rem]) = R.wr[i];
+            }
+        }
+        const bool div = a.in_div != 1.f;
+#pragma unroll
+        for (int i = 0; i < Cfg::XREG; ++i) {
+            const int e = tid + i * kGcNT;
+            if (e < CC * XR * XP) {
+                const int c = e / (XR * XP), rem = e - c * (XR * XP);
+                Xs[c * XCS + rem] = div ? R.xr[i] / a.in_div : R.xr[i];
+            }
+        }
+    };
+
+    f32x4v acc[WM][WN];
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int n = 0; n < WN; ++n) acc[m][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    auto chunk = [&](const int c0, Regs &R) __attribute__((always_inline)) {
+        __syncthreads();  // the previous chunk's LDS reads are done
+        store_chunk(R);
+        __syncthreads();
+#ifndef NLSPN_GC_NOLOAD
+        if (c0 + 2 * CC < ce) load_chunk(c0 + 2 * CC, R);  // in flight while this chunk and the next compute
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        // the chunk's k-steps j = (4-channel group c4, tap t), software pipelined by hand: the
+        // operands of step j + 1 are read while the MFMAs of step j issue (scheduling barriers
+        // keep the compiler from sinking the reads next to their use and then waiting on an LDS
+        // round trip before every MFMA group)
+        constexpr int NS = (CC / 4) * NTAP;
+        float av[2][WM], bv[2][WN];
+        auto fetch = [&](const int j, const int slot) __attribute__((always_inline)) {
+            const int c4 = j / NTAP, t = j % NTAP;
+            int ky, kx, dy, dx;
+            gc_tap<MODE, PH>(t, ky, kx, dy, dx);
+            (void)ky; (void)kx;
+#pragma unroll
+            for (int m = 0; m < WM; ++m) av[slot][m] = Ws[wb + 4 * c4 * WCS + t * WGCO + 16 * m];
+#pragma unroll
+            for (int n = 0; n < WN; ++n) bv[slot][n] = Xs[xb[n] + 4 * c4 * XCS + dy * XP + dx];
+        };
+        fetch(0, 0);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int cur = j & 1;
+            if (j + 1 < NS) fetch(j + 1, cur ^ 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < WM; ++m)
+#pragma unroll
+                for (int n = 0; n < WN; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][m], bv[cur][n], acc[m][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    Regs R0, R1;
+    load_chunk(cs, R0);
+    if (cs + CC < ce) load_chunk(cs + CC, R1);
+    for (int c0 = cs; c0 < ce; c0 += 2 * CC) {
+        chunk(c0, R0);
+        if (c0 + CC < ce) chunk(c0 + CC, R1);
+    }
+
+    // epilogue: lane l, register r of block (m, n) holds output channel co = co0 + 16 m + 4 (l >> 4) + r
+    // of this lane's pixel of block n.  Per n-block every global operand (bias; GRU: h, z, qx) is
+    // loaded first, then combined and stored: one memory round trip per block, not per element.
+    // Lanes past the grid or the crop use an in-range pixel and skip the store.
+    const int co0 = cot * WGCO + wm * (16 * WM);
+    const long long HWo = (long long)a.Ho * a.Wo;
+    float bv[WM][4];
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[m][r] = a.bias[co0 + 16 * m + 4 * lg + r];  // (padded to the co tiles)
+    const int hc = a.hc;
+    const int gate = EPI == kGcEpiGru1 ? (cot * WGCO) / hc : 0;  // GRU1: 0 z, 1 r, 2 qx (uniform per tile)
+#pragma unroll
+    for (int n = 0; n < WN; ++n) {
+        const int gy = gyv[n], gx = gxv[n];
+        int oy = gy, ox = gx;
+        if constexpr (MODE == kGcT2) {
+            oy = 2 * gy + (PH >> 1);
+            ox = 2 * gx + (PH & 1);
+        }
+        const bool ok = gy < a.gh && oy < a.ohs && ox < a.ows;
+        const long long pix = ok ? (long long)oy * a.Wo + ox : 0;
+        if constexpr (EPI == kGcEpiAct) {
+            const long long pixs = ok ? (long long)oy * a.ows + ox : 0;
+            const long long HWs = (long long)a.ohs * a.ows;
+#pragma unroll
+            for (int m = 0; m < WM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = co0 + 16 * m + 4 * lg + r;
+                    float u = acc[m][n][r] + bv[m][r];
+                    if (a.act == kGcActRelu) u = u < 0.f ? 0.f : u;  // (NaN kept, as torch's ReLU)
+                    else if (a.act == kGcActTanh) u = tanhf(u);
+                    if (ok && co < a.cout) a.y[((long long)b * a.cout + co) * HWs + pixs] = u;
+                }
+        } else if constexpr (EPI == kGcEpiGru1) {
+            float hv[WM][4];
+            const long long ob = ((long long)b * hc + (co0 - gate * hc)) * HWo + pix;  // channel co0 of the gate
+            if (gate == 1) {
+#pragma unroll
+                for (int m = 0; m < WM; ++m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hv[m][r] = a.h[ob + (long long)(16 * m + 4 * lg + r) * HWo];
+            }
+            float *dst = gate == 0 ? a.zb : gate == 1 ? a.rhb : a.qxb;
+#pragma unroll
+            for (int m = 0; m < WM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float u = acc[m][n][r] + bv[m][r];
+                    float o;
+                    if (gate == 0) o = 1.f / (1.f + expf(-u));                    // z
+                    else if (gate == 1) o = (1.f / (1.f + expf(-u))) * hv[m][r];  // r * h
+                    else o = u;                                                    // convq's x half + bias
+                    if (ok) dst[ob + (long long)(16 * m + 4 * lg + r) * HWo] = o;
+                }
+        } else {  // kGcEpiGru2
+            float qv[WM][4], zv[WM][4], hv[WM][4];
+            const long long ob = ((long long)b * hc + co0) * HWo + pix;
+#pragma unroll
+            for (int m = 0; m < WM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const long long o = ob + (long long)(16 * m + 4 * lg + r) * HWo;
+                    qv[m][r] = a.qxb[o];
+                    zv[m][r] = a.zb[o];
+                    hv[m][r] = a.h[o];
+                }
+#pragma unroll
+            for (int m = 0; m < WM; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float q = tanhf(acc[m][n][r] + qv[m][r]);
+                    const float z = zv[m][r];
+                    if (ok) a.hout[ob + (long long)(16 * m + 4 * lg + r) * HWo] = (1.f - z) * hv[m][r] + z * q;  // :402
+                }
+        }
+    }
+}
+
+template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI>
+__global__ void __launch_bounds__(kGcNT) gconv_kernel(GconvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float gc_lds[];
+    const int per_phase = a.co_tiles * a.B * a.nbands * a.tpb;
+    const int nph = MODE == kGcT2 ? 4 : 1;
+    const int wg = xcd_remap((int)blockIdx.x, per_phase * nph);  // neighbouring tiles (and co tiles) share an XCD
+    const int ph = wg / per_phase, wgi = wg - ph * per_phase;
+    if constexpr (MODE == kGcT2) {
+        switch (ph) {
+            case 0: gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 0>(a, gc_lds, wgi); break;
+            case 1: gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 1>(a, gc_lds, wgi); break;
+            case 2: gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 2>(a, gc_lds, wgi); break;
+            default: gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 3>(a, gc_lds, wgi); break;
+        }
+    } else {
+        gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 0>(a, gc_lds, wgi);
+    }
+}
+
+// The instantiated configurations: X(id, MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI).  Ids 0..5 are the
+// presets NLSPN_GC_* of include/nlspn_prop.h; ids >= 16 are alternative tilings of the same
+// layer kinds, selectable through nlspn_gconv's layer argument for A/B timing
+// (tools/gc_bench.py) and bit-compatible with the preset of their kind in layout (the packed
+// weights depend only on the kind's output-channel tile).
+#define NLSPN_GC_CONFIGS(X)                                        \
+    X(0, kGcS2, 4, 1, 1, 4, 12, 72, 8, kGcEpiAct)                  \
+    X(1, kGcS2, 1, 2, 1, 4, 16, 72, 8, kGcEpiAct)                  \
+    X(2, kGcS1, 4, 2, 2, 2, 8, 72, 8, kGcEpiGru1)                  \
+    X(3, kGcS1, 4, 2, 2, 2, 8, 72, 8, kGcEpiGru2)                  \
+    X(4, kGcT2, 4, 1, 1, 4, 8, 72, 8, kGcEpiAct)                   \
+    X(5, kGcT2, 1, 4, 1, 4, 12, 72, 8, kGcEpiAct)                  \
+    X(16, kGcS1, 4, 2, 2, 2, 8, 40, 16, kGcEpiGru1)                \
+    X(17, kGcS1, 4, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
+    X(18, kGcS1, 4, 4, 2, 1, 8, 40, 16, kGcEpiGru1)                \
+    X(19, kGcS1, 4, 2, 2, 2, 8, 40, 16, kGcEpiGru2)                \
+    X(20, kGcS2, 4, 1, 1, 4, 12, 72, 16, kGcEpiAct)                \
+    X(21, kGcS2, 4, 2, 1, 2, 12, 72, 16, kGcEpiAct)                \
+    X(22, kGcT2, 4, 1, 1, 4, 6, 40, 16, kGcEpiAct)                 \
+    X(23, kGcT2, 4, 2, 1, 2, 6, 40, 16, kGcEpiAct)                 \
+    X(24, kGcT2, 1, 4, 1, 4, 8, 80, 16, kGcEpiAct)                 \
+    X(25, kGcT2, 1, 2, 1, 4, 8, 80, 16, kGcEpiAct)
+
+}  // namespace nlspn

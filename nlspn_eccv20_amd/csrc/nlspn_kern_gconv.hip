@@ -1,0 +1,8 @@
+// Device code of the GRU-mode convolutions (nlspn_gconv.h), their own translation unit.
+// Launched from nlspn_capi.hip (nlspn_gconv); the configurations are NLSPN_GC_CONFIGS.
+#include "nlspn_gconv.h"
+
+namespace nlspn {
+#define NLSPN_GC_INST(id, ...) template __global__ void gconv_kernel<__VA_ARGS__>(GconvArgs);
+NLSPN_GC_CONFIGS(NLSPN_GC_INST)
+}  // namespace nlspn

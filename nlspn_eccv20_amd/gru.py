@@ -1,0 +1,220 @@
+"""GRU-mode convolutions on the HIP kernels (the reference's forced
+default mode, src/config.py:225-228).
+
+One GRU-mode iteration of the reference (src/model/nlspnmodel.py:365-373) runs, per
+iteration after the first,
+    dep_feat = encode_dep(new_pred / max_depth)          (:366, modules :134-138)
+    aff_feat = encode_aff(aff)            (first update)   (:368-369, :127-132)
+    aff_feat = GRU(h=aff_feat, x=dep_feat)               (:371, ConvGRU :386-403)
+    aff      = _aff_head(aff_feat)                       (:373, decode_aff :140-143 + _clip_as)
+``GruConvs`` runs every one of those convolutions as ``nlspn_gconv`` launches
+(``csrc/nlspn_gconv.h``): f32-input MFMA implicit GEMMs reading NCHW in place, bias and
+ReLU / Tanh / the GRU's sigmoid-tanh-blend in their epilogues, the crop written directly —
+9 launches per iteration where the module path issues ~40 (convolutions, bias adds, ReLUs,
+cats, sigmoids, tanh, blends, layout copies).  Numerics: exact f32 products and f32
+accumulation; only the summation order differs from MIOpen's (RMSE vs the reference's
+GRU-mode fixtures well inside their 1e-4 bar, tests/test_gpu_gru.py).
+
+Inference only (no autograd formula): NLSPNModel uses it when gradients are off; training
+keeps the torch modules.  Weights are packed once per weight version into the kernels'
+layout and cached (``GruConvs.pack``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+__all__ = ["GruConvs", "GC_S2", "GC_S2_C16", "GC_GRU1", "GC_GRU2", "GC_T2", "GC_T2_C16"]
+
+GC_S2, GC_S2_C16, GC_GRU1, GC_GRU2, GC_T2, GC_T2_C16 = range(6)
+ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+# the transposed conv's taps per output phase (py, px), in the kernel's order
+# (nlspn_gconv.h gc_tap): ky = 1 (py = 0) or 0, 2 (py = 1); likewise kx
+_T_TAPS = [[(ky, kx) for ky in ((0, 2) if py else (1,)) for kx in ((0, 2) if px else (1,))]
+           for py in (0, 1) for px in (0, 1)]
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _layout(layer):
+    co, cc, tr = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.get().nlspn_gconv_pack_layout(layer, ctypes.byref(co), ctypes.byref(cc), ctypes.byref(tr)))
+    return co.value, cc.value, bool(tr.value)
+
+
+def pack_conv(weight: torch.Tensor, bias: torch.Tensor, layer: int):
+    """(Cout, Cin, 3, 3) conv weight -> [co_tile][cin_pad][9][co_tile_width]; bias padded."""
+    wgco, cc, tr = _layout(layer)
+    assert not tr
+    cout, cin = weight.shape[:2]
+    ct = (cout + wgco - 1) // wgco
+    cp = (cin + cc - 1) // cc * cc
+    w = torch.zeros((ct * wgco, cp, 9), device=weight.device, dtype=torch.float32)
+    w[:cout, :cin] = weight.detach().float().reshape(cout, cin, 9)
+    w = w.reshape(ct, wgco, cp, 9).permute(0, 2, 3, 1).contiguous()
+    b = torch.zeros(ct * wgco, device=weight.device, dtype=torch.float32)
+    if bias is not None:
+        b[:cout] = bias.detach().float()
+    return w.reshape(-1), b
+
+
+def pack_convt(weight: torch.Tensor, bias: torch.Tensor, layer: int):
+    """(Cin, Cout, 3, 3) transposed-conv weight -> per output phase [co_tile][cin_pad][ntap][width],
+    the phases one after another; bias padded."""
+    wgco, cc, tr = _layout(layer)
+    assert tr
+    cin, cout = weight.shape[:2]
+    ct = (cout + wgco - 1) // wgco
+    cp = (cin + cc - 1) // cc * cc
+    wd = weight.detach().float()
+    parts = []
+    for taps in _T_TAPS:
+        w = torch.zeros((ct * wgco, cp, len(taps)), device=weight.device, dtype=torch.float32)
+        for t, (ky, kx) in enumerate(taps):
+            w[:cout, :cin, t] = wd[:, :, ky, kx].t()
+        parts.append(w.reshape(ct, wgco, cp, len(taps)).permute(0, 2, 3, 1).contiguous().reshape(-1))
+    b = torch.zeros(ct * wgco, device=weight.device, dtype=torch.float32)
+    if bias is not None:
+        b[:cout] = bias.detach().float()
+    return torch.cat(parts), b
+
+
+def _conv_of(seq):
+    return seq[0] if isinstance(seq, nn.Sequential) else seq
+
+
+def _has_relu(seq):
+    return isinstance(seq, nn.Sequential) and any(isinstance(m, nn.ReLU) for m in seq)
+
+
+class _Layer:
+    __slots__ = ("layer", "w", "b", "cin", "cout", "act")
+
+    def __init__(self, layer, w, b, cin, cout, act):
+        self.layer, self.w, self.b, self.cin, self.cout, self.act = layer, w, b, cin, cout, act
+
+
+class GruConvs:
+    """The packed GRU-mode convolutions of one NLSPNModel (encode_dep, encode_aff, ConvGRU,
+    decode_aff), one entry per device, rebuilt when any parameter changes (storage pointer
+    or version counter)."""
+
+    def __init__(self):
+        self._entries = {}
+
+    @staticmethod
+    def supported(model) -> bool:
+        """The reference's GRU-mode architecture (nlspnmodel.py:122-143): 3x3 convs, stride 2
+        encoders, stride-2 transposed decoders, a ConvGRU with hidden channels a multiple of
+        128, float32 CUDA weights."""
+        if not getattr(model.args, "use_GRU", False):
+            return False
+        hc = model.args.GRU_hidden_dim
+        if hc % 128 != 0 or model.args.GRU_input_dim != hc:
+            return False
+        convs = [_conv_of(s) for s in list(model.encode_dep) + list(model.encode_aff)[:3]]
+        convts = [_conv_of(s) for s in model.decode_aff]
+        for c in convs:
+            if not isinstance(c, nn.Conv2d) or c.kernel_size != (3, 3) or c.stride != (2, 2) or c.padding != (1, 1) \
+                    or c.bias is None or c.groups != 1 or c.dilation != (1, 1):
+                return False
+        for c in convts:
+            if not isinstance(c, nn.ConvTranspose2d) or c.kernel_size != (3, 3) or c.stride != (2, 2) \
+                    or c.padding != (1, 1) or c.output_padding != (1, 1) or c.bias is None or c.groups != 1:
+                return False
+        g = model.GRU
+        w = g.convz.weight
+        return w.is_cuda and w.dtype == torch.float32
+
+    def pack(self, model):
+        params = [p for m in (model.encode_dep, model.encode_aff, model.GRU, model.decode_aff) for p in m.parameters()]
+        key = (params[0].device, tuple((p.data_ptr(), p._version) for p in params))
+        e = self._entries.get(params[0].device)
+        if e is not None and e[0] == key:
+            return e[1]
+        with torch.no_grad():
+            enc = lambda seq: [_Layer(GC_S2_C16 if _conv_of(s).out_channels <= 16 else GC_S2,  # noqa: E731
+                                      *pack_conv(_conv_of(s).weight, _conv_of(s).bias,
+                                                 GC_S2_C16 if _conv_of(s).out_channels <= 16 else GC_S2),
+                                      _conv_of(s).in_channels, _conv_of(s).out_channels,
+                                      ACT_RELU if _has_relu(s) else ACT_NONE) for s in seq]
+            dep = enc(list(model.encode_dep))
+            aff = enc(list(model.encode_aff)[:3])
+            aff[-1].act = ACT_TANH  # encode_aff's Tanh (:131)
+            dec = [_Layer(GC_T2_C16 if _conv_of(s).out_channels <= 16 else GC_T2,
+                          *pack_convt(_conv_of(s).weight, _conv_of(s).bias,
+                                      GC_T2_C16 if _conv_of(s).out_channels <= 16 else GC_T2),
+                          _conv_of(s).in_channels, _conv_of(s).out_channels,
+                          ACT_RELU if _has_relu(s) else ACT_NONE) for s in model.decode_aff]
+            g = model.GRU
+            w1 = torch.cat([g.convz.weight, g.convr.weight, g.convq.weight], 0)
+            b1 = torch.cat([g.convz.bias, g.convr.bias, g.convq.bias], 0)
+            hc = g.convz.out_channels
+            gru1 = _Layer(GC_GRU1, *pack_conv(w1, b1, GC_GRU1), 2 * hc, 3 * hc, ACT_NONE)
+            gru2 = _Layer(GC_GRU2, *pack_conv(g.convq.weight[:, :hc], g.convq.bias, GC_GRU2), hc, hc, ACT_NONE)
+        packed = {"dep": dep, "aff": aff, "dec": dec, "gru1": gru1, "gru2": gru2, "hc": hc}
+        self._entries[params[0].device] = (key, packed)
+        return packed
+
+    # ------------------------------------------------------------------ launches
+    @staticmethod
+    def _run(L, x0, c0, x1=None, c1=0, out=None, ohs=None, ows=None, in_div=1.0, h=None, zb=None, rhb=None,
+             qxb=None, hout=None, hc=0):
+        B, _, Hi, Wi = x0.shape
+        lib = _lib.get()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(x0.device).cuda_stream)
+        _lib.check(lib.nlspn_gconv(L.layer, _p(x0), c0, _p(x1), c1, _p(L.w), _p(L.b), _p(out), _p(h), _p(zb), _p(rhb),
+                                   _p(qxb), _p(hout), B, Hi, Wi, L.cout, ohs or 0, ows or 0, L.act,
+                                   ctypes.c_float(in_div), hc, stream))
+
+    def _conv_s2(self, L, x, in_div=1.0):
+        B, _, Hi, Wi = x.shape
+        Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
+        y = torch.empty((B, L.cout, Ho, Wo), device=x.device, dtype=torch.float32)
+        self._run(L, x, L.cin, out=y, ohs=Ho, ows=Wo, in_div=in_div)
+        return y
+
+    def _convt(self, L, x, crop=None):
+        B, _, Hi, Wi = x.shape
+        Ho, Wo = 2 * Hi, 2 * Wi
+        ohs, ows = (min(crop[0], Ho), min(crop[1], Wo)) if crop else (Ho, Wo)
+        y = torch.empty((B, L.cout, ohs, ows), device=x.device, dtype=torch.float32)
+        self._run(L, x, L.cin, out=y, ohs=ohs, ows=ows)
+        return y
+
+    def encode_dep(self, P, new_pred, max_depth):
+        """encode_dep(new_pred / max_depth) (:366): the division in the first conv's loads."""
+        x = new_pred.contiguous().float()
+        for i, L in enumerate(P["dep"]):
+            x = self._conv_s2(L, x, in_div=float(max_depth) if i == 0 else 1.0)
+        return x
+
+    def encode_aff(self, P, aff):
+        x = aff.contiguous().float()
+        for L in P["aff"]:
+            x = self._conv_s2(L, x)
+        return x
+
+    def gru(self, P, h, x):
+        """ConvGRU (:398-403): h' = (1 - z) h + z q."""
+        h, x = h.contiguous(), x.contiguous()
+        hc = P["hc"]
+        z, rh, qx = (torch.empty_like(h) for _ in range(3))
+        hn = torch.empty_like(h)
+        self._run(P["gru1"], h, hc, x, x.shape[1], h=h, zb=z, rhb=rh, qxb=qx, hc=hc)
+        self._run(P["gru2"], rh, hc, h=h, zb=z, qxb=qx, hout=hn, hc=hc)
+        return hn
+
+    def decode_aff(self, P, h, crop):
+        """decode_aff + _clip_as (:228-250): the last layer stores only the cropped rows / columns."""
+        x = h
+        n = len(P["dec"])
+        for i, L in enumerate(P["dec"]):
+            x = self._convt(L, x, crop=crop if i == n - 1 else None)
+        return x

@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from .propagation import (affinity_normalization, kernel_geometry, off_insert, prop_step, propagate,
                           propagate_normalized)
+from .gru import GruConvs
 from .heads import HeadWeights, head_epilogue, head_epilogue_prologue
 from .s2d import s2d_front
 
@@ -247,6 +248,10 @@ class NLSPNModel(nn.Module):
         if args.use_S2D:
             self.S2D = S2D()
         self._head_weights = HeadWeights()  # packed head-epilogue weights (a cache, not state)
+        # GRU mode at inference: encode_dep / encode_aff / ConvGRU / decode_aff as HIP
+        # convolutions (gru.py); False keeps the torch modules (A/B, tests)
+        self.native_gru = True
+        self._gru_convs = GruConvs()
         params = nn.ParameterList([p for p in self.parameters() if p.requires_grad])
         self.param_groups = [{"params": params, "lr": args.lr}]
 
@@ -324,6 +329,10 @@ class NLSPNModel(nn.Module):
 
     def _aff_head(self, aff_feat):
         """nlspnmodel.py:228-234 (+ the _clip_as crop :237-250)."""
+        if self._native_gru(aff_feat):
+            gc = self._gru_convs
+            aff = gc.decode_aff(gc.pack(self), aff_feat, (self.args.patch_height, self.args.patch_width))
+            return affinity_normalization(aff, self.aff_scale_const, self.args.affinity)
         aff = self.decode_aff(aff_feat)
         aff = aff[:, :, :self.args.patch_height, :self.args.patch_width].contiguous()
         return affinity_normalization(aff, self.aff_scale_const, self.args.affinity)
@@ -406,9 +415,22 @@ class NLSPNModel(nn.Module):
         return {"pred": pred, "pred_init": pred_init, "pred_inter": list_pred, "offset": o["offset"], "aff": aff,
                 "gamma": self.aff_scale_const.data, "confidence": conf_eff}
 
+    def _native_gru(self, x):
+        """The GRU-mode convolutions run on the HIP kernels (gru.py): inference on CUDA with the
+        reference's GRU architecture; training keeps the torch modules (their autograd)."""
+        return (self.native_gru and x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.float32
+                and GruConvs.supported(self))
+
     def _gru_update(self, aff_feat, aff, new_pred, k):
         """nlspnmodel.py:365-371: encode the new depth, (at the first update) encode the
         affinity, one ConvGRU step."""
+        if self._native_gru(new_pred):
+            gc = self._gru_convs
+            P = gc.pack(self)
+            dep_feat = gc.encode_dep(P, new_pred, self.args.max_depth)
+            if k == 2:
+                aff_feat = gc.encode_aff(P, aff)
+            return gc.gru(P, aff_feat, dep_feat)
         dep_feat = self.encode_dep(new_pred / self.args.max_depth)
         if k == 2:
             aff_feat = self.encode_aff(aff)

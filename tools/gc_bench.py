@@ -1,0 +1,107 @@
+"""Per-layer timing of the GRU-mode convolutions (nlspn_gconv, csrc/nlspn_gconv.h) at a bench
+config's shapes: every layer kind under its preset and the alternative tilings of
+NLSPN_GC_CONFIGS (ids >= 16), interleaved in the same process; outputs checked bit-equal
+to the preset's (the k order per output is the same under every tiling).  Prints JSON:
+per layer and config id the median us per launch and TF/s of useful FLOPs.
+usage: python tools/gc_bench.py [--B 8 --H 228 --W 304] [--reps 20]"""
+import argparse
+import json
+import os
+import sys
+import types
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nlspn_eccv20_amd import NLSPNModel  # noqa: E402
+from nlspn_eccv20_amd import gru as G  # noqa: E402
+
+KINDS = {"s2": (G.GC_S2, [20, 21]), "s2c16": (G.GC_S2_C16, []), "gru1": (G.GC_GRU1, [16, 17, 18]),
+         "gru2": (G.GC_GRU2, [19]), "t2": (G.GC_T2, [22, 23]), "t2c16": (G.GC_T2_C16, [24, 25])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=8)
+    ap.add_argument("--H", type=int, default=228)
+    ap.add_argument("--W", type=int, default=304)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--presets-only", action="store_true")
+    a = ap.parse_args()
+    dev = "cuda:0"
+    B, H, W = a.B, a.H, a.W
+    args = types.SimpleNamespace(prop_kernel=3, affinity="TGASS", affinity_gamma=0.5, prop_time=18,
+                                 preserve_input=True, always_clip=False, conf_prop=True, offset=True,
+                                 network="resnet34", from_scratch=True, zero_init_aff=False, use_GRU=True,
+                                 use_S2D=False, GRU_hidden_dim=128, GRU_input_dim=128, lr=1e-3, max_depth=10.0,
+                                 patch_height=H, patch_width=W, model_name="NLSPN")
+    torch.manual_seed(0)
+    m = NLSPNModel(args).to(dev).eval()
+    gc = G.GruConvs()
+    P = gc.pack(m)
+    g = torch.Generator(device=dev).manual_seed(1)
+    r = lambda *s: torch.rand(s, device=dev, generator=g)  # noqa: E731
+    h1, w1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    h2, w2 = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
+    h3, w3 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
+    hc = 128
+    h, x = r(B, hc, h3, w3), r(B, hc, h3, w3)
+    z, rh, qx, hn = (torch.empty_like(h) for _ in range(4))
+    # (name, kind, packed layer, inputs (x0, c0, x1, c1), output shape / crop, useful flops)
+    layers = [
+        ("enc1", "s2c16", P["dep"][0], (r(B, 1, H, W), 1, None, 0), (B, 16, h1, w1), 2 * B * h1 * w1 * 16 * 9),
+        ("enc2", "s2", P["dep"][1], (r(B, 16, h1, w1), 16, None, 0), (B, 256, h2, w2), 2 * B * h2 * w2 * 256 * 16 * 9),
+        ("enc3", "s2", P["dep"][2], (r(B, 256, h2, w2), 256, None, 0), (B, 128, h3, w3), 2 * B * h3 * w3 * 128 * 256 * 9),
+        ("gru1", "gru1", P["gru1"], (h, hc, x, hc), None, 2 * B * h3 * w3 * (256 * 256 * 9 + 128 * 128 * 9)),
+        ("gru2", "gru2", P["gru2"], (rh, hc, None, 0), None, 2 * B * h3 * w3 * 128 * 128 * 9),
+        ("convt1", "t2", P["dec"][0], (r(B, 128, h3, w3), 128, None, 0), (B, 256, 2 * h3, 2 * w3),
+         2 * B * (2 * h3) * (2 * w3) * 256 * 128 * 9 / 4),
+        ("convt2", "t2c16", P["dec"][1], (r(B, 256, 2 * h3, 2 * w3), 256, None, 0), (B, 16, 4 * h3, 4 * w3),
+         2 * B * (4 * h3) * (4 * w3) * 16 * 256 * 9 / 4),
+        ("convt3", "t2c16", P["dec"][2], (r(B, 16, 4 * h3, 4 * w3), 16, None, 0), (B, 8, H, W),
+         2 * B * H * W * 8 * 16 * 9 / 4),
+    ]
+    out = {"B": B, "H": H, "W": W, "layers": {}}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for name, kind, L, (x0, c0, x1, c1), oshape, flops in layers:
+        ids = [KINDS[kind][0]] + ([] if a.presets_only else KINDS[kind][1])
+        res, ref = {}, None
+        for cid in ids:
+            L2 = G._Layer(cid, L.w, L.b, L.cin, L.cout, L.act)
+            y = torch.empty(oshape, device=dev) if oshape else None
+
+            def run():
+                if kind == "gru1":
+                    G.GruConvs._run(L2, x0, c0, x1, c1, h=h, zb=z, rhb=rh, qxb=qx, hc=hc)
+                    return torch.cat([z, rh, qx])
+                if kind == "gru2":
+                    G.GruConvs._run(L2, x0, c0, h=h, zb=z, qxb=qx, hout=hn, hc=hc)
+                    return hn
+                G.GruConvs._run(L2, x0, c0, x1, c1, out=y, ohs=oshape[2], ows=oshape[3])
+                return y
+            try:
+                o = run().clone()
+            except Exception as ex:  # noqa: BLE001
+                res[cid] = {"error": str(ex)[:200]}
+                continue
+            if ref is None:
+                ref = o
+            same = bool(torch.equal(o.view(torch.int32), ref.view(torch.int32)))
+            ts = []
+            for _ in range(3):
+                run()
+            for _ in range(a.reps):
+                e0.record()
+                run()
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            ts.sort()
+            us = ts[len(ts) // 2]
+            res[cid] = {"us": round(us, 1), "tflops": round(flops / (us * 1e-6) / 1e12, 1), "bit_equal_preset": same}
+        out["layers"][name] = res
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
