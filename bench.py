@@ -181,8 +181,9 @@ def roofline(name, cfg, resident, first_ms, rest_ms, ms_per_step):
     elif resident:
         kname, kmean = "prop_resident_kernel", rest_ms
         # reads: K normalised affinities (tap K/2 is recomputed), 2K offsets, conf', dep, p_1;
-        # writes: pred_inter[1..T-1] and pred
-        comp_planes = (K + 2 * K + 2 + 1) + (T - 1 + 1)
+        # writes: pred_inter[1..T-1], pred and the output dict's 2(K+1) inserted-offset planes
+        # (the resident loop copies them, one plane per iteration: ResArgs::off_out)
+        comp_planes = (K + 2 * K + 2 + 1) + (T - 1 + 1) + 2 * (K + 1)
         alg_iters = T - 1
         kdesc = (f"{kname} (iterations 2..{T}, invariant planes on chip: {resident} launch(es), the full "
                  f"image groups in turn inside one; kernel_ms_mean spans them all)")

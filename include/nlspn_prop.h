@@ -409,6 +409,9 @@ int nlspn_resident_status(int clear);
 #define NLSPN_GC_GRU2 3
 #define NLSPN_GC_T2 4
 #define NLSPN_GC_T2_C16 5
+/* the narrow first encoder convs on the VALU: wpk is then the module's own (16, cin, 3, 3)
+ * weight tensor (cin <= 16) and bias its own (16) */
+#define NLSPN_GC_S2_SMALL 6
 #define NLSPN_GC_ACT_NONE 0
 #define NLSPN_GC_ACT_RELU 1
 #define NLSPN_GC_ACT_TANH 2

@@ -69,6 +69,7 @@ extern template __global__ void heads_kernel<1, false, 0, true>(HeadsArgs);
 // defined in nlspn_kern_gconv.hip
 #define NLSPN_GC_EXTERN(id, ...) extern template __global__ void gconv_kernel<__VA_ARGS__>(GconvArgs);
 NLSPN_GC_CONFIGS(NLSPN_GC_EXTERN)
+extern template __global__ void gsmall_kernel<16>(GconvArgs, const float *);
 }  // namespace nlspn
 
 using namespace nlspn;
@@ -1616,6 +1617,12 @@ bool gc_get(int layer, GcPreset &p) {
 extern "C" {
 
 int nlspn_gconv_pack_layout(int layer, int *co_tile, int *cin_chunk, int *transposed) {
+    if (layer == NLSPN_GC_S2_SMALL) {  // the module's own weight layout
+        if (co_tile) *co_tile = 0;
+        if (cin_chunk) *cin_chunk = 1;
+        if (transposed) *transposed = 0;
+        return NLSPN_OK;
+    }
     GcPreset p;
     if (!gc_get(layer, p)) return fail(NLSPN_EINVAL, "unknown GRU-mode conv preset %d", layer);
     if (co_tile) *co_tile = p.wgco;
@@ -1627,6 +1634,26 @@ int nlspn_gconv_pack_layout(int layer, int *co_tile, int *cin_chunk, int *transp
 int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk, const float *bias,
                 float *y, const float *h, float *zb, float *rhb, float *qxb, float *hout, int B, int Hi, int Wi,
                 int cout, int ohs, int ows, int act, float in_div, int hc, void *stream) {
+    if (layer == NLSPN_GC_S2_SMALL) {
+        // (the kernel reads the module's own (16, cin, 3, 3) tensor)
+        if (B < 1 || Hi < 1 || Wi < 1 || c0 < 1 || c1 != 0 || cout != 16 || c0 * 16 * 9 > kGsMaxW)
+            return fail(NLSPN_EINVAL, "gconv small: cin %d (c1 %d), cout %d outside the VALU kernel's range (cout 16, "
+                        "cin <= 16)", c0, c1, cout);
+        if (!x0 || !wpk || !bias || !y) return fail(NLSPN_EINVAL, "gconv small: null pointer");
+        GconvArgs a{};
+        a.x0 = x0; a.bias = bias; a.y = y; a.c0 = c0; a.B = B; a.Hi = Hi; a.Wi = Wi;
+        a.Ho = (Hi - 1) / 2 + 1;
+        a.Wo = (Wi - 1) / 2 + 1;
+        a.ohs = ohs; a.ows = ows; a.cout = cout; a.act = act; a.in_div = in_div;
+        if (ohs < 1 || ows < 1 || ohs > a.Ho || ows > a.Wo)
+            return fail(NLSPN_EINVAL, "gconv small: stored size %dx%d outside the output %dx%d", ohs, ows, a.Ho, a.Wo);
+        const long long npix = (long long)B * ohs * ows;
+        const unsigned grid = (unsigned)std::min<long long>((npix + kGsNT - 1) / kGsNT, 1 << 20);
+        void *args[] = {&a, const_cast<float **>(&wpk)};
+        NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&gsmall_kernel<16>), dim3(grid), dim3(kGsNT), args,
+                                      0, as_stream(stream)));
+        return check_launch("nlspn_gconv small");
+    }
     GcPreset p;
     if (!gc_get(layer, p)) return fail(NLSPN_EINVAL, "unknown GRU-mode conv preset %d", layer);
     if (B < 1 || Hi < 1 || Wi < 1 || cout < 1 || c0 < 1 || c1 < 0 || (c1 > 0 && !x1))

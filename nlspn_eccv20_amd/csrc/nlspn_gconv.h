@@ -90,7 +90,8 @@ struct GcCfg {
     // 16 banks apart), input window [CC][XR][XP] (+16 per channel)
     static constexpr int WCS = NTMAX * WGCO + 16;
     static constexpr int XCS = XR * XP + 16;
-    static constexpr int LDS_FLOATS = CC * WCS + CC * XCS;
+    static constexpr int STAGE = CC * WCS + CC * XCS;  // one LDS stage (weights + window of a chunk)
+    static constexpr int LDS_FLOATS = 2 * STAGE;        // two stages: chunk k computes while k + 1 is stored
     static constexpr int WREG = (CC * NTMAX * WGCO + kGcNT - 1) / kGcNT;   // prefetch registers (weights)
     static constexpr int XREG = (CC * XR * XP + kGcNT - 1) / kGcNT;     // prefetch registers (window)
 };
@@ -101,6 +102,7 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
     constexpr int WGCO = Cfg::WGCO, NPX = Cfg::NPX, WCS = Cfg::WCS, XCS = Cfg::XCS;
     constexpr int NTAP = gc_ntap(MODE, PH);
     constexpr int S = MODE == kGcS2 ? 2 : 1;
+    // stage s: weights at lds + s STAGE, window after them
     float *Ws = lds;
     float *Xs = lds + CC * WCS;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -197,13 +199,14 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
         for (int i = 0; i < Cfg::XREG; ++i)
             R.xr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, xoff[i], 0u, 0));
     };
-    auto store_chunk = [&](const Regs &R) __attribute__((always_inline)) {
+    auto store_chunk = [&](const Regs &R, const int stage) __attribute__((always_inline)) {
+        float *Wd = Ws + stage * Cfg::STAGE, *Xd = Xs + stage * Cfg::STAGE;
 #pragma unroll
         for (int i = 0; i < WR4; ++i) {
             const int e = tid + i * kGcNT;
             if (e < WF4) {
                 const int c = (4 * e) / (NTAP * WGCO), rem = 4 * e - c * (NTAP * WGCO);
-                *reinterpret_cast<f32x4 *>(&Ws[c * WCS + rem]) = R.wr[i];
+                *reinterpret_cast<f32x4 *>(&Wd[c * WCS + rem]) = R.wr[i];
             }
         }
         const bool div = a.in_div != 1.f;
@@ -212,7 +215,7 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
             const int e = tid + i * kGcNT;
             if (e < CC * XR * XP) {
                 const int c = e / (XR * XP), rem = e - c * (XR * XP);
-                Xs[c * XCS + rem] = div ? R.xr[i] / a.in_div : R.xr[i];
+                Xd[c * XCS + rem] = div ? R.xr[i] / a.in_div : R.xr[i];
             }
         }
     };
@@ -223,14 +226,12 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
 #pragma unroll
         for (int n = 0; n < WN; ++n) acc[m][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-    auto chunk = [&](const int c0, Regs &R) __attribute__((always_inline)) {
-        __syncthreads();  // the previous chunk's LDS reads are done
-        store_chunk(R);
-        __syncthreads();
-#ifndef NLSPN_GC_NOLOAD
-        if (c0 + 2 * CC < ce) load_chunk(c0 + 2 * CC, R);  // in flight while this chunk and the next compute
-#endif
-        __builtin_amdgcn_sched_barrier(0);
+    // The chunk loop: one barrier per chunk.  Chunk k computes from stage k & 1 while its
+    // waves then store chunk k + 1 (loaded one chunk earlier: the loads had chunk k's MFMAs to
+    // land) into the other stage — last read by chunk k - 1, which every wave finished before
+    // the previous barrier — and issue chunk k + 2's loads.
+    auto compute = [&](const int stage) __attribute__((always_inline)) {
+        const float *Wc = Ws + stage * Cfg::STAGE, *Xc = Xs + stage * Cfg::STAGE;
         // the chunk's k-steps j = (4-channel group c4, tap t), software pipelined by hand: the
         // operands of step j + 1 are read while the MFMAs of step j issue (scheduling barriers
         // keep the compiler from sinking the reads next to their use and then waiting on an LDS
@@ -243,9 +244,9 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
             gc_tap<MODE, PH>(t, ky, kx, dy, dx);
             (void)ky; (void)kx;
 #pragma unroll
-            for (int m = 0; m < WM; ++m) av[slot][m] = Ws[wb + 4 * c4 * WCS + t * WGCO + 16 * m];
+            for (int m = 0; m < WM; ++m) av[slot][m] = Wc[wb + 4 * c4 * WCS + t * WGCO + 16 * m];
 #pragma unroll
-            for (int n = 0; n < WN; ++n) bv[slot][n] = Xs[xb[n] + 4 * c4 * XCS + dy * XP + dx];
+            for (int n = 0; n < WN; ++n) bv[slot][n] = Xc[xb[n] + 4 * c4 * XCS + dy * XP + dx];
         };
         fetch(0, 0);
 #pragma unroll
@@ -261,12 +262,22 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    Regs R0, R1;
-    load_chunk(cs, R0);
-    if (cs + CC < ce) load_chunk(cs + CC, R1);
-    for (int c0 = cs; c0 < ce; c0 += 2 * CC) {
-        chunk(c0, R0);
-        if (c0 + CC < ce) chunk(c0 + CC, R1);
+    Regs R;
+    load_chunk(cs, R);
+    store_chunk(R, 0);
+    if (cs + CC < ce) load_chunk(cs + CC, R);
+    __syncthreads();
+    auto step = [&](const int c0, const int stage) __attribute__((always_inline)) {
+        compute(stage);
+        if (c0 + CC < ce) {
+            store_chunk(R, stage ^ 1);
+            if (c0 + 2 * CC < ce) load_chunk(c0 + 2 * CC, R);
+        }
+        __syncthreads();
+    };
+    for (int c0 = cs; c0 < ce; c0 += 2 * CC) {  // (two chunks per trip: the stages are compile-time)
+        step(c0, 0);
+        if (c0 + CC < ce) step(c0 + CC, 1);
     }
 
     // epilogue: lane l, register r of block (m, n) holds output channel co = co0 + 16 m + 4 (l >> 4) + r
@@ -369,27 +380,69 @@ __global__ void __launch_bounds__(kGcNT) gconv_kernel(GconvArgs a) {
     }
 }
 
+// The narrow first layers (encode_dep / encode_aff's first conv: 1 or 9 -> 16 channels) on the
+// VALU: one thread per output pixel holds the 16 sums, reads its taps' inputs directly and the
+// weights as LDS broadcasts.  As MFMA tiles their K (9 or 81 terms) would be mostly padding and
+// their windows mostly empty; here they are bound by their few MB of HBM traffic (NYU B=8:
+// 16 vs 34 us).  Same bias / activation epilogue.  (The 16 -> 8 transposed conv measured
+// slower this way — per-lane output phases diverge — and stays on the MFMA kernel.)
+constexpr int kGsNT = 256, kGsMaxW = 16 * 16 * 9;  // threads; weights held in LDS (16 x cin x 9 at most)
+template <int COUT>
+__global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float *w) {
+    // w: the module's own (cout, cin, 3, 3) layout
+    __shared__ float ws[kGsMaxW];
+    const int cin = a.c0;
+    for (int i = threadIdx.x; i < COUT * cin * 9; i += kGsNT) ws[i] = w[i];
+    __syncthreads();
+    const long long npix = (long long)a.B * a.ohs * a.ows;
+    const long long HWi = (long long)a.Hi * a.Wi;
+    for (long long p = (long long)blockIdx.x * kGsNT + threadIdx.x; p < npix; p += (long long)gridDim.x * kGsNT) {
+        const int b = (int)(p / ((long long)a.ohs * a.ows));
+        const int rem = (int)(p - (long long)b * a.ohs * a.ows);
+        const int oy = rem / a.ows, ox = rem - oy * a.ows;
+        float acc[COUT];
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[co] = 0.f;
+        const float *xb = a.x0 + (long long)b * cin * HWi;
+        for (int ci = 0; ci < cin; ++ci) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const int iy = 2 * oy - 1 + ky;
+                if ((unsigned)iy >= (unsigned)a.Hi) continue;
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const int ix = 2 * ox - 1 + kx;
+                    if ((unsigned)ix >= (unsigned)a.Wi) continue;
+                    float v = xb[(long long)ci * HWi + (long long)iy * a.Wi + ix];
+                    if (a.in_div != 1.f) v = v / a.in_div;
+#pragma unroll
+                    for (int co = 0; co < COUT; ++co) acc[co] = fmaf(ws[(co * cin + ci) * 9 + ky * 3 + kx], v, acc[co]);
+                }
+            }
+        }
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) {
+            float u = acc[co] + a.bias[co];
+            if (a.act == kGcActRelu) u = u < 0.f ? 0.f : u;
+            else if (a.act == kGcActTanh) u = tanhf(u);
+            a.y[(((long long)b * a.cout + co) * a.ohs + oy) * a.ows + ox] = u;
+        }
+    }
+}
+
 // The instantiated configurations: X(id, MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI).  Ids 0..5 are the
 // presets NLSPN_GC_* of include/nlspn_prop.h; ids >= 16 are alternative tilings of the same
 // layer kinds, selectable through nlspn_gconv's layer argument for A/B timing
 // (tools/gc_bench.py) and bit-compatible with the preset of their kind in layout (the packed
-// weights depend only on the kind's output-channel tile).
+// weights depend only on the kind's output-channel tile, which a variant must keep).
 #define NLSPN_GC_CONFIGS(X)                                        \
-    X(0, kGcS2, 4, 1, 1, 4, 12, 72, 8, kGcEpiAct)                  \
-    X(1, kGcS2, 1, 2, 1, 4, 16, 72, 8, kGcEpiAct)                  \
-    X(2, kGcS1, 4, 2, 2, 2, 8, 72, 8, kGcEpiGru1)                  \
-    X(3, kGcS1, 4, 2, 2, 2, 8, 72, 8, kGcEpiGru2)                  \
-    X(4, kGcT2, 4, 1, 1, 4, 8, 72, 8, kGcEpiAct)                   \
-    X(5, kGcT2, 1, 4, 1, 4, 12, 72, 8, kGcEpiAct)                  \
-    X(16, kGcS1, 4, 2, 2, 2, 8, 40, 16, kGcEpiGru1)                \
-    X(17, kGcS1, 4, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
-    X(18, kGcS1, 4, 4, 2, 1, 8, 40, 16, kGcEpiGru1)                \
-    X(19, kGcS1, 4, 2, 2, 2, 8, 40, 16, kGcEpiGru2)                \
-    X(20, kGcS2, 4, 1, 1, 4, 12, 72, 16, kGcEpiAct)                \
-    X(21, kGcS2, 4, 2, 1, 2, 12, 72, 16, kGcEpiAct)                \
-    X(22, kGcT2, 4, 1, 1, 4, 6, 40, 16, kGcEpiAct)                 \
-    X(23, kGcT2, 4, 2, 1, 2, 6, 40, 16, kGcEpiAct)                 \
-    X(24, kGcT2, 1, 4, 1, 4, 8, 80, 16, kGcEpiAct)                 \
-    X(25, kGcT2, 1, 2, 1, 4, 8, 80, 16, kGcEpiAct)
+    X(0, kGcS2, 4, 1, 1, 4, 12, 40, 8, kGcEpiAct)                  \
+    X(1, kGcS2, 1, 1, 1, 4, 10, 72, 8, kGcEpiAct)                  \
+    X(2, kGcS1, 2, 2, 2, 2, 8, 40, 8, kGcEpiGru1)                  \
+    X(3, kGcS1, 2, 2, 2, 2, 8, 40, 8, kGcEpiGru2)                  \
+    X(4, kGcT2, 4, 1, 1, 4, 6, 40, 8, kGcEpiAct)                   \
+    X(5, kGcT2, 1, 4, 1, 4, 6, 80, 8, kGcEpiAct)                   \
+    X(16, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
+    X(17, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru2)
 
 }  // namespace nlspn

@@ -5,4 +5,5 @@
 namespace nlspn {
 #define NLSPN_GC_INST(id, ...) template __global__ void gconv_kernel<__VA_ARGS__>(GconvArgs);
 NLSPN_GC_CONFIGS(NLSPN_GC_INST)
+template __global__ void gsmall_kernel<16>(GconvArgs, const float *);
 }  // namespace nlspn

@@ -11,7 +11,8 @@ iteration after the first,
 (``csrc/nlspn_gconv.h``): f32-input MFMA implicit GEMMs reading NCHW in place, bias and
 ReLU / Tanh / the GRU's sigmoid-tanh-blend in their epilogues, the crop written directly —
 9 launches per iteration where the module path issues ~40 (convolutions, bias adds, ReLUs,
-cats, sigmoids, tanh, blends, layout copies).  Numerics: exact f32 products and f32
+cats, sigmoids, tanh, blends, layout copies).  The 1- / 9-channel first encoder convs run on a
+VALU kernel (as MFMA tiles their K would be mostly padding).  Numerics: exact f32 products and f32
 accumulation; only the summation order differs from MIOpen's (RMSE vs the reference's
 GRU-mode fixtures well inside their 1e-4 bar, tests/test_gpu_gru.py).
 
@@ -28,9 +29,9 @@ import torch.nn as nn
 
 from . import _lib
 
-__all__ = ["GruConvs", "GC_S2", "GC_S2_C16", "GC_GRU1", "GC_GRU2", "GC_T2", "GC_T2_C16"]
+__all__ = ["GruConvs", "GC_S2", "GC_S2_C16", "GC_GRU1", "GC_GRU2", "GC_T2", "GC_T2_C16", "GC_S2_SMALL"]
 
-GC_S2, GC_S2_C16, GC_GRU1, GC_GRU2, GC_T2, GC_T2_C16 = range(6)
+GC_S2, GC_S2_C16, GC_GRU1, GC_GRU2, GC_T2, GC_T2_C16, GC_S2_SMALL = range(7)
 ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
 # the transposed conv's taps per output phase (py, px), in the kernel's order
 # (nlspn_gconv.h gc_tap): ky = 1 (py = 0) or 0, 2 (py = 1); likewise kx
@@ -132,6 +133,12 @@ class GruConvs:
         w = g.convz.weight
         return w.is_cuda and w.dtype == torch.float32
 
+    @staticmethod
+    def _raw(layer, conv, act):
+        """A narrow layer for the VALU kernel: the module's own weight layout."""
+        return _Layer(layer, conv.weight.detach().float().contiguous(), conv.bias.detach().float().contiguous(),
+                      conv.in_channels, conv.out_channels, act)
+
     def pack(self, model):
         params = [p for m in (model.encode_dep, model.encode_aff, model.GRU, model.decode_aff) for p in m.parameters()]
         key = (params[0].device, tuple((p.data_ptr(), p._version) for p in params))
@@ -146,6 +153,11 @@ class GruConvs:
                                       ACT_RELU if _has_relu(s) else ACT_NONE) for s in seq]
             dep = enc(list(model.encode_dep))
             aff = enc(list(model.encode_aff)[:3])
+            # the first (1 / 9 -> 16 channel) convs on the VALU kernel
+            for lst, seq in ((dep, model.encode_dep), (aff, model.encode_aff)):
+                c = _conv_of(seq[0])
+                if c.out_channels == 16 and c.in_channels <= 16:
+                    lst[0] = self._raw(GC_S2_SMALL, c, lst[0].act)
             aff[-1].act = ACT_TANH  # encode_aff's Tanh (:131)
             dec = [_Layer(GC_T2_C16 if _conv_of(s).out_channels <= 16 else GC_T2,
                           *pack_convt(_conv_of(s).weight, _conv_of(s).bias,
