@@ -220,8 +220,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return base + slot;
 }
 
-// Inverse of xcd_remap: the block index that xcd_remap maps to logical index L.
+// Inverse of xcd_remap: the block index that xcd_remap maps to logical index L.  L is clamped
+// into [0, nblk): the resident kernel indexes its sync lines by the result, and an index from
+// outside the grid (a negative neighbour band, the likely cause of round 5's one
+// illegal-address fault in a dropped neighbour-wait form) must not address
+// past the workspace.  (For nblk < kNumXcd the else branch would divide by q = 0.)
 __device__ __forceinline__ int xcd_unmap(int L, int nblk) {
+    L = min(max(L, 0), nblk - 1);
     const int q = nblk / kNumXcd, r = nblk % kNumXcd;
     int xcd, slot;
     if (L < r * (q + 1)) {
