@@ -398,7 +398,8 @@ int nlspn_resident_status(int clear);
  * nlspn_gconv_pack_layout's layout (nlspn_eccv20_amd/gru.py packs them), bias padded to
  * the co tiles.  NLSPN_GC_S2* / NLSPN_GC_T2*: y = act(conv + bias) stored as (B, cout, ohs,
  * ows) (ohs / ows <= the full output size: the crop), act NLSPN_GC_ACT_*, inputs divided by
- * in_div while read (encode_dep's new_pred / max_depth; 1: none).  NLSPN_GC_GRU1 (x0 = h, x1
+ * in_div while read (encode_dep's new_pred / max_depth; 1: none; != 1 only with
+ * NLSPN_GC_S2_SMALL, else NLSPN_EINVAL).  NLSPN_GC_GRU1 (x0 = h, x1
  * = x, cout = 3 hc): z, r*h and qx (convq's x half + bias) into zb / rhb / qxb;
  * NLSPN_GC_GRU2 (x0 = rhb, c1 = 0, cout = hc): h' = (1 - z) h + z tanh(convq's r*h half +
  * qx) into hout.  Returns NLSPN_EUNSUPPORTED when a shape's window does not fit the kernel.

@@ -1659,6 +1659,9 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     if (B < 1 || Hi < 1 || Wi < 1 || cout < 1 || c0 < 1 || c1 < 0 || (c1 > 0 && !x1))
         return fail(NLSPN_EINVAL, "gconv: bad shape B=%d Hi=%d Wi=%d c0=%d c1=%d cout=%d", B, Hi, Wi, c0, c1, cout);
     if (!x0 || !wpk || !bias) return fail(NLSPN_EINVAL, "gconv: null input, weights or bias");
+    // (the MFMA kernels stage their inputs by LDS-DMA, untouched: a divided input is the VALU
+    // kernel's, NLSPN_GC_S2_SMALL)
+    if (in_div != 1.f) return fail(NLSPN_EINVAL, "gconv: in_div %g needs the NLSPN_GC_S2_SMALL preset", (double)in_div);
     const bool gru = p.epi != kGcEpiAct, gru1 = p.epi == kGcEpiGru1;
     GconvArgs a{};
     a.x0 = x0; a.x1 = x1; a.w = wpk; a.bias = bias; a.y = y;

@@ -23,8 +23,8 @@
 // row-major runs of NPX pixels — no tile columns wasted on a 38-pixel-wide 1/8-scale image.
 // Per chunk of CC input channels the workgroup stages the packed weights [ci][tap][co] and
 // the input window (the rows / columns its pixels' taps reach, zero outside the image = the
-// zero padding) in LDS; the next chunk's global loads are in flight in registers while the
-// current chunk computes.  The LDS window pitch XP is a compile-time constant, so every
+// zero padding) in LDS by LDS-DMA loads (no staging registers, no LDS store instructions);
+// the next chunk's loads land in the other LDS stage while the current chunk computes.  The LDS window pitch XP is a compile-time constant, so every
 // operand read is one ds_read_b32 with an immediate offset from a per-lane base.
 #pragma once
 
@@ -55,7 +55,7 @@ struct GconvArgs {
     int bw, nbands, tpb;   // band width, bands, tiles per band (of the widest band)
     int npx;               // pixels per tile (<= NPX: a narrow band's tile must fit the window rows)
     int act;               // kGcAct*
-    float in_div;          // inputs divided by it while staged (encode_dep: max_depth, :366); 1: as they are
+    float in_div;          // inputs divided by it (encode_dep: max_depth, :366): the VALU kernel only, 1 for the MFMA kernels
     int hc;                // GRU hidden channels
 };
 
@@ -82,29 +82,41 @@ __device__ __forceinline__ constexpr void gc_tap(int t, int &ky, int &kx, int &d
     }
 }
 
+// LDS channel strides.  The four lane groups (k rows) of an operand read sit one channel
+// stride apart; a ds_read_b32 serves lanes 0-31 and 32-63 in turn over 32 banks, so groups 0 / 1
+// (and 2 / 3) must not share banks: a weight row or a stride-1 window row (16 consecutive
+// words) needs a stride = 16 (mod 32), a stride-2 window row (16 even words) an odd stride.
+__host__ __device__ constexpr int gc_wcs(int ntap, int wgco) { return ntap * wgco + (16 - (ntap * wgco) % 32 + 32) % 32; }
+__host__ __device__ constexpr int gc_xcs(int mode, int xr, int xp) {
+    return mode == kGcS2 ? xr * xp + 1 - (xr * xp) % 2 : xr * xp + (16 - (xr * xp) % 32 + 32) % 32;
+}
+__host__ __device__ constexpr int gc_round(int v, int m) { return (v + m - 1) / m * m; }
+
 template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI>
 struct GcCfg {
     static constexpr int WGCO = 16 * WM * WGM, NPX = 16 * WN * WGN;
     static constexpr int NTMAX = MODE == kGcT2 ? 4 : 9;
-    // LDS: weights [CC][NTMAX][WGCO] (+16 floats per channel: the four lane groups' rows start
-    // 16 banks apart), input window [CC][XR][XP] (+16 per channel)
-    static constexpr int WCS = NTMAX * WGCO + 16;
-    static constexpr int XCS = XR * XP + 16;
-    static constexpr int STAGE = CC * WCS + CC * XCS;  // one LDS stage (weights + window of a chunk)
-    static constexpr int LDS_FLOATS = 2 * STAGE;        // two stages: chunk k computes while k + 1 is stored
-    static constexpr int WREG = (CC * NTMAX * WGCO + kGcNT - 1) / kGcNT;   // prefetch registers (weights)
-    static constexpr int XREG = (CC * XR * XP + kGcNT - 1) / kGcNT;     // prefetch registers (window)
+    static constexpr int XCS = gc_xcs(MODE, XR, XP);
+    // One LDS stage = a chunk's weights [CC][WCS] then its input window [CC][XCS], each region
+    // rounded up to whole LDS-DMA rounds of the workgroup (256 lanes x 16 B weights, x 4 B
+    // window: every lane's write lands inside the stage).
+    static constexpr int WST = gc_round(CC * gc_wcs(NTMAX, WGCO), 4 * kGcNT);
+    static constexpr int XST = gc_round(CC * XCS, kGcNT);
+    static constexpr int STAGE = WST + XST;
+    static constexpr int LDS_FLOATS = 2 * STAGE;  // two stages: chunk k computes while k + 1 lands
+    static constexpr int WREG = WST / (4 * kGcNT), XREG = XST / kGcNT;  // LDS-DMA loads per lane per chunk
 };
 
 template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI, int PH>
 __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int wgi) {
     using Cfg = GcCfg<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI>;
-    constexpr int WGCO = Cfg::WGCO, NPX = Cfg::NPX, WCS = Cfg::WCS, XCS = Cfg::XCS;
+    constexpr int WGCO = Cfg::WGCO, NPX = Cfg::NPX, XCS = Cfg::XCS;
     constexpr int NTAP = gc_ntap(MODE, PH);
+    constexpr int WCS = gc_wcs(NTAP, WGCO);  // (this phase's taps only)
     constexpr int S = MODE == kGcS2 ? 2 : 1;
     // stage s: weights at lds + s STAGE, window after them
     float *Ws = lds;
-    float *Xs = lds + CC * WCS;
+    float *Xs = lds + Cfg::WST;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv % WGM, wn = wv / WGM;
     const int l16 = lane & 15, lg = lane >> 4;
@@ -153,38 +165,39 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
     constexpr int TAP0 = MODE == kGcT2 ? (PH == 0 ? 0 : PH == 1 ? 1 : PH == 2 ? 3 : 5) : 0;
     const float *wsrc = a.w + (long long)a.cin_pad * WGCO * ((long long)TAP0 * a.co_tiles + (long long)cot * NTAP);
 
-    // Staging.  The window cells a thread loads are the same every chunk, only the channels
-    // change: each cell's byte offset within a chunk's channels is computed once (0x80000000
-    // for a cell outside the window or the image: the buffer load returns 0 = the zero
-    // padding), and a chunk is one buffer descriptor whose size ends at the source's last
-    // channel (channels past it, the chunk's padding, read 0 too).  The weights of a chunk
-    // are contiguous: 16-byte loads.
-    constexpr int WF4 = CC * NTAP * WGCO / 4;  // float4s of a chunk's weights
-    constexpr int WR4 = (WF4 + kGcNT - 1) / kGcNT;
+    // Staging: LDS-DMA (buffer / global loads that write LDS directly, no registers).  Lane l
+    // of wave w's i-th load writes stage word (i * 256 + 64 w + l) (x 4 words for the weights),
+    // so the source of every LDS position is computed once: a window word's byte offset within
+    // a chunk's channels (0x80000000 for a pad word or a cell outside the window or the image:
+    // the buffer load returns 0 = the zero padding; a chunk is one buffer descriptor whose size
+    // ends at the source's last channel, so the chunk's padding channels read 0 too), a weight
+    // quad's float offset within the chunk's contiguous weights (pad quads reload quad 0 into
+    // the pad: never read).
     unsigned xoff[Cfg::XREG];
 #pragma unroll
     for (int i = 0; i < Cfg::XREG; ++i) {
-        const int e = tid + i * kGcNT;
-        const int c = e / (XR * XP), rem = e - c * (XR * XP);
+        const int p = tid + i * kGcNT;
+        const int c = p / XCS, rem = p - c * XCS;
         const int row = rem / XP, col = rem - row * XP;
         const int iy = iy0 + row, ix = ix0 + col;
-        const bool ok = c < CC && row < nrows && col < ncols && (unsigned)iy < (unsigned)a.Hi &&
+        const bool ok = c < CC && rem < XR * XP && row < nrows && col < ncols && (unsigned)iy < (unsigned)a.Hi &&
                         (unsigned)ix < (unsigned)a.Wi;
         xoff[i] = ok ? (unsigned)(((long long)c * HWi + (long long)iy * a.Wi + ix) * 4) : 0x80000000u;
     }
-    // two register sets: chunk k + 2's loads are issued while chunk k computes, so a load has
-    // two chunks' MFMAs to land (one chunk's, at one wave per SIMD, left L2 latency exposed)
-    struct Regs {
-        f32x4 wr[WR4];
-        float xr[Cfg::XREG];
-    };
-    auto load_chunk = [&](int c0, Regs &R) __attribute__((always_inline)) {
-        const rsrc_t rw = make_rsrc(wsrc + (long long)c0 * NTAP * WGCO);
+    int woff[Cfg::WREG];
 #pragma unroll
-        for (int i = 0; i < WR4; ++i) {
-            const int e = min(tid + i * kGcNT, WF4 - 1);
-            R.wr[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)e * 16u, 0u, 0));
-        }
+    for (int i = 0; i < Cfg::WREG; ++i) {
+        const int p = 4 * (tid + i * kGcNT);
+        const int c = p / WCS, rem = p - c * WCS;
+        woff[i] = c < CC && rem < NTAP * WGCO ? c * NTAP * WGCO + rem : 0;
+    }
+    typedef __attribute__((address_space(3))) void lds_t;
+    auto issue_chunk = [&](int c0, const int stage) __attribute__((always_inline)) {
+        const float *wc = wsrc + (long long)c0 * NTAP * WGCO;
+        float *Wd = Ws + stage * Cfg::STAGE + 4 * 64 * wv, *Xd = Xs + stage * Cfg::STAGE + 64 * wv;
+#pragma unroll
+        for (int i = 0; i < Cfg::WREG; ++i)
+            __builtin_amdgcn_global_load_lds(wc + woff[i], (lds_t *)(Wd + 4 * kGcNT * i), 16, 0, 0);
         // (a chunk past the last channel — possible only within the 16-channel packing pad, which
         // the loop bound below excludes — would read nothing: an empty descriptor on x0)
         const bool s0 = c0 < a.c0;
@@ -197,27 +210,7 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
         const rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, nrec, 0x00020000);
 #pragma unroll
         for (int i = 0; i < Cfg::XREG; ++i)
-            R.xr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, xoff[i], 0u, 0));
-    };
-    auto store_chunk = [&](const Regs &R, const int stage) __attribute__((always_inline)) {
-        float *Wd = Ws + stage * Cfg::STAGE, *Xd = Xs + stage * Cfg::STAGE;
-#pragma unroll
-        for (int i = 0; i < WR4; ++i) {
-            const int e = tid + i * kGcNT;
-            if (e < WF4) {
-                const int c = (4 * e) / (NTAP * WGCO), rem = 4 * e - c * (NTAP * WGCO);
-                *reinterpret_cast<f32x4 *>(&Wd[c * WCS + rem]) = R.wr[i];
-            }
-        }
-        const bool div = a.in_div != 1.f;
-#pragma unroll
-        for (int i = 0; i < Cfg::XREG; ++i) {
-            const int e = tid + i * kGcNT;
-            if (e < CC * XR * XP) {
-                const int c = e / (XR * XP), rem = e - c * (XR * XP);
-                Xd[c * XCS + rem] = div ? R.xr[i] / a.in_div : R.xr[i];
-            }
-        }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_t *)(Xd + kGcNT * i), 4, xoff[i], 0, 0, 0);
     };
 
     f32x4v acc[WM][WN];
@@ -226,10 +219,6 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
 #pragma unroll
         for (int n = 0; n < WN; ++n) acc[m][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-    // The chunk loop: one barrier per chunk.  Chunk k computes from stage k & 1 while its
-    // waves then store chunk k + 1 (loaded one chunk earlier: the loads had chunk k's MFMAs to
-    // land) into the other stage — last read by chunk k - 1, which every wave finished before
-    // the previous barrier — and issue chunk k + 2's loads.
     auto compute = [&](const int stage) __attribute__((always_inline)) {
         const float *Wc = Ws + stage * Cfg::STAGE, *Xc = Xs + stage * Cfg::STAGE;
         // the chunk's k-steps j = (4-channel group c4, tap t), software pipelined by hand: the
@@ -262,17 +251,14 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    Regs R;
-    load_chunk(cs, R);
-    store_chunk(R, 0);
-    if (cs + CC < ce) load_chunk(cs + CC, R);
-    __syncthreads();
+    issue_chunk(cs, 0);
+    __syncthreads();  // (waits for the loads: vmcnt(0), then the barrier)
+    // one barrier per chunk: chunk k + 1's loads go to the other stage — last read by chunk
+    // k - 1, which every wave finished before the previous barrier — and land while chunk k
+    // computes; the barrier after it waits for them.
     auto step = [&](const int c0, const int stage) __attribute__((always_inline)) {
+        if (c0 + CC < ce) issue_chunk(c0 + CC, stage ^ 1);
         compute(stage);
-        if (c0 + CC < ce) {
-            store_chunk(R, stage ^ 1);
-            if (c0 + 2 * CC < ce) load_chunk(c0 + 2 * CC, R);
-        }
         __syncthreads();
     };
     for (int c0 = cs; c0 < ce; c0 += 2 * CC) {  // (two chunks per trip: the stages are compile-time)
