@@ -422,13 +422,17 @@ __global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float 
 // (tools/gc_bench.py) and bit-compatible with the preset of their kind in layout (the packed
 // weights depend only on the kind's output-channel tile, which a variant must keep).
 #define NLSPN_GC_CONFIGS(X)                                        \
-    X(0, kGcS2, 4, 1, 1, 4, 12, 40, 8, kGcEpiAct)                  \
+    X(0, kGcS2, 4, 1, 1, 4, 12, 40, 4, kGcEpiAct)                  \
     X(1, kGcS2, 1, 1, 1, 4, 10, 72, 8, kGcEpiAct)                  \
-    X(2, kGcS1, 2, 2, 2, 2, 8, 40, 8, kGcEpiGru1)                  \
+    X(2, kGcS1, 2, 2, 2, 2, 6, 40, 4, kGcEpiGru1)                  \
     X(3, kGcS1, 2, 2, 2, 2, 8, 40, 8, kGcEpiGru2)                  \
     X(4, kGcT2, 4, 1, 1, 4, 6, 40, 8, kGcEpiAct)                   \
     X(5, kGcT2, 1, 4, 1, 4, 6, 80, 8, kGcEpiAct)                   \
-    X(16, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
-    X(17, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru2)
+    X(16, kGcS1, 2, 2, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
+    X(17, kGcS1, 2, 2, 2, 2, 6, 40, 4, kGcEpiGru2)                 \
+    X(18, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
+    X(20, kGcS2, 4, 1, 1, 4, 12, 40, 8, kGcEpiAct)                 \
+    X(21, kGcT2, 4, 1, 1, 4, 6, 40, 4, kGcEpiAct)                  \
+    X(22, kGcT2, 1, 4, 1, 4, 6, 80, 4, kGcEpiAct)
 
 }  // namespace nlspn
