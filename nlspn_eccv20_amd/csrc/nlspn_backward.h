@@ -146,7 +146,8 @@ __device__ __forceinline__ float aff_norm_backward(const float (&G)[K], const fl
 // for K <= 8 — the dL/daff and dL/doffset accumulators.  Larger K accumulate in
 // registers and read-modify-write in chunks of 8 planes.
 // DIAG: diagnostic knobs for tools/bwd_bench (0 in the library; non-zero values
-// produce wrong gradients): 1 = no window flush, 4 = no accumulator read-modify-write.
+// produce wrong gradients): 1 = no window flush, 4 = no accumulator read-modify-write,
+// 8 = no scatter at all (SPLIT: neither the LDS window adds nor the direct atomics).
 // SPLIT (two-pass form, offsets): the step only produces dL/dout (written to go_out) and
 // scatters dL/df_{t-1}; the dL/daff and dL/doffset terms, which need f_{t-1} at every
 // tap, are computed for all T iterations afterwards by bwd_coef_kernel.  Without the
@@ -363,7 +364,8 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
         };
         if (exact) add_win((ly + RY) * WW + lx + RX, go * aref);  // reference tap: integer point, weight 1
         else atomicAdd(&gfw[y * W + x], go * aref);
-        if constexpr (SPLIT) {
+        if constexpr (SPLIT && (DIAG & 8)) {
+        } else if constexpr (SPLIT) {
             // scatter only: the corner weights of every valid tap (.cuh:196-254)
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -528,7 +530,9 @@ struct BwdCoefArgs {
     unsigned flags;
 };
 
-template <int KH, int KW, int TH, int TW, int RY, int RX, int SV>
+// CW: conf' (iteration-invariant) is staged into an LDS window once; iterations t >= 2 then
+// load only p_{t-1} and form f = p * conf' from it (half the staging loads).
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool CW = false>
 __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel(BwdCoefArgs a) {
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
@@ -539,6 +543,7 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
     static_assert(RY > PH && RX > PW, "window must cover the tap base grid");
     static_assert(SV == 1 || (RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
     __shared__ __attribute__((aligned(16))) float win[WH * WW];
+    __shared__ __attribute__((aligned(16))) float cwin[CW ? WH * WW : 4];
     __shared__ float red[NT / 64];
 
     const int H = a.H, W = a.W;
@@ -572,6 +577,27 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
     }
     const rsrc_t rgo = make_rsrc(a.g_off + b * a.goff_bs);
     const rsrc_t rgr = make_rsrc(a.grad_aff_raw + b * a.gaff_bs);
+    const bool cw = CW && has_conf;  // (conf_prop off: f = p, nothing to keep)
+    if (cw) {  // conf' over the window (zero outside the image), once
+        const rsrc_t rc = make_rsrc(a.conf_eff + b * HW);
+#pragma unroll
+        for (int it = 0; it < SIT; ++it) {
+            const int i = threadIdx.x + it * NT;
+            const int ii = i < NV ? i : NV - 1;
+            const int r = ii / WV, c = (ii - r * WV) * SV;
+            int gy = wy0 + r, gx = wx0 + c;
+            const bool in = i < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            gy = gy < 0 ? 0 : (gy > H - 1 ? H - 1 : gy);
+            gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
+            float v[SV];
+            BVec<float, SV>::load(rc, (unsigned)(gy * W + gx) * ES, 0u, v);
+            if (i < NV) {
+#pragma unroll
+                for (int e = 0; e < SV; ++e) cwin[r * WW + c + e] = in ? v[e] : 0.f;
+            }
+        }
+        // (each thread reads back only the cells it wrote: the staging below maps cells alike)
+    }
 
     const auto iter = [&](auto first_c, int t) {
         constexpr bool FIRST = decltype(first_c)::value;
@@ -593,7 +619,7 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
             gx = gx < 0 ? 0 : (gx > W - SV ? W - SV : gx);
             const unsigned q = (unsigned)(gy * W + gx) * ES;
             BVec<float, SV>::load(rp, q, 0u, sp[it]);
-            if (has_conf) BVec<float, SV>::load(rc, q, 0u, sc[it]);
+            if (has_conf && (FIRST || !cw)) BVec<float, SV>::load(rc, q, 0u, sc[it]);
             if (FIRST && preserve) BVec<float, SV>::load(rd, q, 0u, sd[FIRST ? it : 0]);
         }
         // this iteration's dL/dout at the own pixel (plane t-1 of the dL/dout store)
@@ -606,13 +632,15 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
             const int i = threadIdx.x + it * NT;
             if (i < NV) {
                 float v[SV];
+                const int r = i / WV, c = (i - r * WV) * SV;
 #pragma unroll
                 for (int e = 0; e < SV; ++e) {
-                    const float f = make_f<FIRST>(sp[it][e], has_conf ? sc[it][e] : 1.f,
-                                                  FIRST && preserve ? sd[FIRST ? it : 0][e] : 0.f, has_conf, preserve, clip);
+                    // (cw: conf' from the LDS window, the same product p * conf')
+                    const float cc = has_conf ? (!FIRST && cw ? cwin[r * WW + c + e] : sc[it][e]) : 1.f;
+                    const float f = make_f<FIRST>(sp[it][e], cc, FIRST && preserve ? sd[FIRST ? it : 0][e] : 0.f,
+                                                  has_conf, preserve, clip);
                     v[e] = sin[it] ? f : 0.f;
                 }
-                const int r = i / WV, c = (i - r * WV) * SV;
                 if constexpr (SV == 4)
                     *reinterpret_cast<float4 *>(&win[r * WW + c]) = make_float4(v[0], v[1], v[2], v[3]);
                 else

@@ -17,6 +17,7 @@
 #include "nlspn_mdcn.h"
 #include "nlspn_affnorm.h"
 #include "nlspn_backward.h"
+#include "nlspn_bwd_resident.h"
 #include "nlspn_step.h"
 #include "nlspn_resident.h"
 #include "nlspn_s2d.h"
@@ -745,6 +746,62 @@ unsigned elementwise_grid(long long groups) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
+// ---- resident pass 1 of the two-pass backward (nlspn_bwd_resident.h)
+// Parts: images of one launch x (py x px) rectangles of PR x PC pixels, at most one part per CU
+// (every part co-resident), PR * PC <= kBrNT * kBrPX pixels, the LDS window within kBrMaxCells.
+// The most images per launch (fewest launches), then the most parts, then the shortest
+// perimeter (the halo flush is the window's rim).
+struct BrPlan {
+    int Bl = 0, py = 0, px = 0, PR = 0, PC = 0;
+};
+
+bool br_plan(int B, int H, int W, int cus, BrPlan &P) {
+    const int cap = std::min(cus, kBrMaxParts);
+    for (int Bl = std::min(B, cap); Bl >= 1; --Bl) {
+        const int ppi_max = cap / Bl;
+        BrPlan best;
+        long long best_n = 0, best_per = 0;
+        for (int py = 1; py <= std::min(H, ppi_max); ++py) {
+            const int PR = (H + py - 1) / py;
+            if ((long long)(py - 1) * PR >= H) continue;  // no empty part row
+            for (int px = 1; px <= std::min(W, ppi_max / py); ++px) {
+                const int PC = (W + px - 1) / px;
+                if ((long long)(px - 1) * PC >= W) continue;
+                if ((long long)PR * PC > (long long)kBrNT * kBrPX) continue;
+                const long long cells = (long long)(PR + 2 * kBrR) * (PC + 2 * kBrR);
+                if (cells > kBrMaxCells || (cells + 1) * 8 + (long long)PR * PC * 32 > kBrLdsBytes) continue;
+                const long long n = (long long)py * px, per = PR + PC;
+                if (n > best_n || (n == best_n && per < best_per)) {
+                    best_n = n; best_per = per;
+                    best.Bl = Bl; best.py = py; best.px = px; best.PR = PR; best.PC = PC;
+                }
+            }
+        }
+        if (best_n > 0) { P = best; return true; }
+    }
+    return false;
+}
+
+// The experiments build only: NLSPN_BWD_RESIDENT=0 keeps the per-iteration step launches (A/B).
+bool br_disabled() {
+    if (!kExperiments) return false;
+    const char *e = getenv("NLSPN_BWD_RESIDENT");  // (read per call: A/B in one process)
+    return e && e[0] == '0';
+}
+
+// Pass 2 keeps conf' in an LDS window (bwd_coef_kernel CW); the experiments build only:
+// NLSPN_BWD_CW=0 stages it every iteration (A/B; read per call).
+bool bwd_coef_cw() {
+    if (!kExperiments) return true;
+    const char *e = getenv("NLSPN_BWD_CW");
+    return !(e && e[0] == '0');
+}
+
+size_t br_sync_offset_words(long long N, int K, long long tiles) {
+    const size_t w = (size_t)N * (3 + K) + (size_t)tiles;
+    return (w + kBrLine - 1) / kBrLine * kBrLine;  // a 128-B line boundary
+}
+
 // The whole section (see nlspn_propagate).  ev (optional, 2*T events): a dispatch-
 // recorded pair around each launch — [0,1] step 1 (an empty interval when the resident
 // launches run the prologue), then [2,3] the resident kernel or [2t, 2t+1] per-iteration
@@ -1286,8 +1343,9 @@ int nlspn_time_prop_step(int dtype, const void *p_in, const void *conf, const vo
 size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw) {
     if (B < 1 || H < 1 || W < 1 || kh < 1 || kw < 1) return 0;
     const size_t N = (size_t)B * H * W, K = (size_t)kh * kw - 1;
-    // dL/df ping-pong, G = dL/daff - dL/daff_ref (K planes), dL/dconf', dL/dgamma partials
-    return sizeof(float) * (N * (2 + K + 1) + (size_t)bwd_tiles(B, H, W));
+    // dL/df ping-pong, G = dL/daff - dL/daff_ref (K planes), dL/dconf', dL/dgamma partials, then
+    // (line-aligned) the resident pass 1's sync words
+    return sizeof(float) * (br_sync_offset_words((long long)N, (int)K, bwd_tiles(B, H, W)) + kBrSyncWords);
 }
 
 int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -1344,7 +1402,61 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     const long long goff_bs = grad_off_bstride ? grad_off_bstride : 2LL * K * HW;
     const long long gaff_bs = grad_aff_bstride ? grad_aff_bstride : (long long)K * HW;
     int rc = NLSPN_OK;
-    for (int t = T; t >= 1; --t) {
+    // Resident pass 1 (nlspn_bwd_resident.h): the two-pass form without the clamp's mask,
+    // T >= 2, when every part of an image group fits on the device at once.
+    BrPlan bp;
+    const bool resident = split && !(flags & NLSPN_ALWAYS_CLIP) && T >= 2 && !br_disabled() &&
+                          br_plan(B, H, W, device_cus(), bp);
+    if (resident) {
+        const void *fn = reinterpret_cast<const void *>(&bwd_res_kernel<kBrPX>);
+        const int WH = bp.PR + 2 * kBrR, WW = bp.PC + 2 * kBrR;
+        const int lds = ((WH * WW + 1) & ~1) * 8 + bp.PR * bp.PC * 32;  // window + the part's affinities
+        if ((rc = set_lds_attr(fn, lds))) return rc;
+        int occ = 0;
+        NLSPN_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBrNT, lds));
+        if (occ < 1) return fail(NLSPN_EUNSUPPORTED, "resident backward: no room for a %d-thread part", kBrNT);
+        unsigned *sync = reinterpret_cast<unsigned *>(ws) + br_sync_offset_words(N, K, bwd_tiles(B, H, W));
+        NLSPN_HIP_TRY(hipMemsetAsync(gf[1], 0, sizeof(float) * N, s));  // (gf[(T-1)&1] is cleared above)
+        NLSPN_HIP_TRY(hipMemsetAsync(gf[0], 0, sizeof(float) * N, s));
+        DevState *d = dev_state();
+        for (int b0 = 0; b0 < B; b0 += bp.Bl) {
+            const int nb = std::min(bp.Bl, B - b0);
+            BwdResArgs r{};
+            r.pred_inter = pi;
+            r.conf_eff = conf ? static_cast<const float *>(conf_eff) : nullptr;
+            r.dep = (flags & NLSPN_PRESERVE_INPUT) ? static_cast<const float *>(dep) : nullptr;
+            r.aff = static_cast<const float *>(aff_norm);
+            r.off = static_cast<const float *>(off_raw);
+            r.g_pred = static_cast<const float *>(grad_pred);
+            r.g_inter = static_cast<const float *>(grad_pred_inter);
+            r.gf = gf[0];
+            r.g_conf = conf ? g_conf : nullptr;
+            r.g_off = static_cast<float *>(grad_off_raw);
+            r.g_aff = static_cast<float *>(grad_aff_raw);
+            r.goff_bs = goff_bs;
+            r.gaff_bs = gaff_bs;
+            r.off_bs = off_bstride;
+            r.N = N;
+            r.sync = sync;
+            r.status = d ? d->dev_status : nullptr;
+            r.b0 = b0; r.H = H; r.W = W; r.T = T;
+            r.py = bp.py; r.px = bp.px; r.PR = bp.PR; r.PC = bp.PC; r.WH = WH; r.WW = WW;
+            r.flags = flags;
+            if (kExperiments) {  // (A/B diagnostics, read per call)
+                const char *e = getenv("NLSPN_BWD_RES_DBG");
+                r.dbg = e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
+            }
+            const unsigned grid = (unsigned)(nb * bp.py * bp.px);
+            if (grid > (unsigned)device_cus() * (unsigned)occ) return fail(NLSPN_EUNSUPPORTED, "resident backward grid too large");
+            NLSPN_HIP_TRY(hipMemsetAsync(sync, 0, sizeof(unsigned) * kBrSyncWords, s));
+            if ((rc = res_guard_before(s))) return rc;
+            void *args[] = {&r};
+            NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(kBrNT), args, (size_t)lds, s));
+            if ((rc = check_launch("nlspn_propagate_backward resident pass 1"))) return rc;
+            if ((rc = res_guard_after(s))) return rc;
+        }
+    }
+    for (int t = T; t >= 1 && !resident; --t) {
         const bool first = t == 1;
         BwdArgs a{};
         a.p_in = first ? static_cast<const float *>(pred_init) : pi + (size_t)(t - 2) * N;
@@ -1412,8 +1524,11 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         c.T = T;
         c.kind = kind;
         c.flags = flags;
-        const void *fn = vec ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4>)
-                             : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1>);
+        const bool cw = bwd_coef_cw();
+        const void *fn = vec ? (cw ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4, true>)
+                                   : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4, false>))
+                             : (cw ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1, true>)
+                                   : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1, false>));
         void *cargs[] = {&c};
         NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)bwd_tiles(B, H, W)), dim3(kBwdTH * kBwdTW), cargs, 0, s));
         if ((rc = check_launch("nlspn_propagate_backward coefficients"))) return rc;

@@ -37,10 +37,26 @@ struct Variant {
     int TH, TW;
 };
 
-template <int TH, int TW, int R, int DIAG>
+template <int TH, int TW, int R, int DIAG, bool SPLIT = false>
 Variant mk(const char *name) {
-    return Variant{name, reinterpret_cast<const void *>(&bwd_step_kernel<3, 3, TH, TW, R, R, 4, true, false, DIAG>), TH,
-                   TW};
+    return Variant{name, reinterpret_cast<const void *>(&bwd_step_kernel<3, 3, TH, TW, R, R, 4, true, false, DIAG, SPLIT>),
+                   TH, TW};
+}
+
+// The two-pass step's planes streamed (29 reads, 3 writes per pixel), no gather or scatter.
+__global__ void __launch_bounds__(256) bwd_split_stream_ceiling(BwdArgs a) {
+    const long long HW = (long long)a.H * a.W;
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (long long)a.B * HW) return;
+    const long long b = g / HW, q = g % HW;
+    constexpr int K = 8;
+    float s = a.p_out[g] + a.conf_eff[g] + a.dep[g] + a.gf_read[g] + a.g_inter[g];
+    const float gc = a.g_conf[g];
+    for (int k = 0; k < K; ++k) s += a.aff[(b * (K + 1) + k) * HW + q];
+    for (int k = 0; k < 2 * K; ++k) s += a.off[b * a.off_bs + k * HW + q];
+    a.g_conf[g] = gc + s;
+    a.gf_read[g] = 0.f;
+    a.go_out[g] = s;
 }
 
 // Same planes, same per-pixel lane mapping, streamed: 56 plane reads, 27 writes.
@@ -103,6 +119,9 @@ int main(int argc, char **argv) {
     a.B = B; a.H = H; a.W = W;
     a.last = 0;
     a.flags = kPreserve;
+    float *go_out = up(plane(N, [] { return 0.f; }));
+    a.go_out = go_out;
+    a.go_bs = (long long)H * W;
 
     std::vector<Variant> vs = {
         mk<8, 32, 8, 0>("8x32 R8 (library)"),
@@ -114,6 +133,10 @@ int main(int argc, char **argv) {
         mk<8, 64, 8, 0>("8x64 R8"),
         mk<16, 64, 8, 0>("16x64 R8"),
         {"stream ceiling (83 planes)", reinterpret_cast<const void *>(&bwd_stream_ceiling), 0, 0},
+        mk<8, 32, 8, 0, true>("SPLIT 8x32 R8 (library)"),
+        mk<8, 32, 8, 1, true>("SPLIT no-flush"),
+        mk<8, 32, 8, 9, true>("SPLIT no-scatter"),
+        {"SPLIT stream ceiling (32 planes)", reinterpret_cast<const void *>(&bwd_split_stream_ceiling), 0, 0},
     };
     const double bytes = 83.0 * 4 * N;
     std::vector<std::vector<float>> ms(vs.size());
