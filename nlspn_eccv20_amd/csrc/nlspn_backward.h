@@ -530,9 +530,12 @@ struct BwdCoefArgs {
     unsigned flags;
 };
 
-// CW: conf' (iteration-invariant) is staged into an LDS window once; iterations t >= 2 then
-// load only p_{t-1} and form f = p * conf' from it (half the staging loads).
-template <int KH, int KW, int TH, int TW, int RY, int RX, int SV, bool CW = false>
+// conf' (iteration-invariant) is staged into an LDS window once; iterations t >= 2 load only
+// p_{t-1} and form f = p * conf' from it (half the staging loads; measured within noise of
+// staging both, profiles/r06/ab_bwd_resident_v1.json).  Issuing the next iteration's p loads
+// before the taps (one register window, 105 VGPRs; or capped at 5 waves, 9 VGPRs spilled)
+// measured 5 % / 2 % slower (profiles/r06/ab_bwd_pf_t18_rejected.json).
+template <int KH, int KW, int TH, int TW, int RY, int RX, int SV>
 __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel(BwdCoefArgs a) {
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
@@ -543,7 +546,7 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
     static_assert(RY > PH && RX > PW, "window must cover the tap base grid");
     static_assert(SV == 1 || (RX % 4 == 0 && WW % 4 == 0), "vector staging alignment");
     __shared__ __attribute__((aligned(16))) float win[WH * WW];
-    __shared__ __attribute__((aligned(16))) float cwin[CW ? WH * WW : 4];
+    __shared__ __attribute__((aligned(16))) float cwin[WH * WW];  // conf', invariant
     __shared__ float red[NT / 64];
 
     const int H = a.H, W = a.W;
@@ -577,7 +580,7 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
     }
     const rsrc_t rgo = make_rsrc(a.g_off + b * a.goff_bs);
     const rsrc_t rgr = make_rsrc(a.grad_aff_raw + b * a.gaff_bs);
-    const bool cw = CW && has_conf;  // (conf_prop off: f = p, nothing to keep)
+    const bool cw = has_conf;  // (conf_prop off: f = p, nothing to keep)
     if (cw) {  // conf' over the window (zero outside the image), once
         const rsrc_t rc = make_rsrc(a.conf_eff + b * HW);
 #pragma unroll
@@ -599,6 +602,44 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
         // (each thread reads back only the cells it wrote: the staging below maps cells alike)
     }
 
+    const auto taps = [&](auto first_c, rsrc_t rp, rsrc_t rc, rsrc_t rd, float go) {
+        constexpr bool FIRST = decltype(first_c)::value;
+        // the taps' geometry is t-invariant: opaque moves keep the compiler from hoisting
+        // every tap's weights and addresses out of the t loop (187 VGPRs, 2 waves per SIMD)
+#pragma unroll
+        for (int k = 0; k < K; ++k) asm volatile("" : "+v"(dh[k]), "+v"(dw[k]));
+        if (active) {
+            const float fown = win[(ly + RY) * WW + lx + RX];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int tt = k < REF ? k : k + 1;
+                const int i = tt / KW, jj = tt % KW;
+                const float hs = (float)(y - PH + i) + dh[k];
+                const float ws = (float)(x - PW + jj) + dw[k];
+                float val = 0.f;
+                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
+                    int hl, wl;
+                    float v[4];
+                    tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf, preserve, clip, hl, wl, v);
+                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+                    val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
+                    float cwh = 0.f, cww = 0.f;
+                    cwh += -1 * hw * v[0];
+                    cwh += -1 * lw * v[1];
+                    cwh += hw * v[2];
+                    cwh += lw * v[3];
+                    cww += -1 * hh * v[0];
+                    cww += hh * v[1];
+                    cww += -1 * lh * v[2];
+                    cww += lh * v[3];
+                    cO[2 * k] += cwh * go * av[k];
+                    cO[2 * k + 1] += cww * go * av[k];
+                }
+                cG[k] += go * (val - fown);
+            }
+        }
+    };
     const auto iter = [&](auto first_c, int t) {
         constexpr bool FIRST = decltype(first_c)::value;
         const float *pbase = FIRST ? a.pred_init + b * HW : a.pred_inter + (size_t)(t - 2) * a.N + b * HW;
@@ -648,41 +689,7 @@ __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel
             }
         }
         lds_barrier();
-        // the taps' geometry is t-invariant: opaque moves keep the compiler from hoisting
-        // every tap's weights and addresses out of the t loop (187 VGPRs, 2 waves per SIMD)
-#pragma unroll
-        for (int k = 0; k < K; ++k) asm volatile("" : "+v"(dh[k]), "+v"(dw[k]));
-        if (active) {
-            const float fown = win[(ly + RY) * WW + lx + RX];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int tt = k < REF ? k : k + 1;
-                const int i = tt / KW, jj = tt % KW;
-                const float hs = (float)(y - PH + i) + dh[k];
-                const float ws = (float)(x - PW + jj) + dw[k];
-                float val = 0.f;
-                if (hs > -1.f && ws > -1.f && hs < Hf && ws < Wf) {
-                    int hl, wl;
-                    float v[4];
-                    tap_corners<FIRST, WH, WW>(hs, ws, wy0, wx0, H, W, win, rp, rc, rd, has_conf, preserve, clip, hl, wl, v);
-                    const float lh = hs - (float)hl, lw = ws - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
-                    const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-                    val = (w1 * v[0] + w2 * v[1] + w3 * v[2] + w4 * v[3]);
-                    float cwh = 0.f, cww = 0.f;
-                    cwh += -1 * hw * v[0];
-                    cwh += -1 * lw * v[1];
-                    cwh += hw * v[2];
-                    cwh += lw * v[3];
-                    cww += -1 * hh * v[0];
-                    cww += hh * v[1];
-                    cww += -1 * lh * v[2];
-                    cww += lh * v[3];
-                    cO[2 * k] += cwh * go * av[k];
-                    cO[2 * k + 1] += cww * go * av[k];
-                }
-                cG[k] += go * (val - fown);
-            }
-        }
+        taps(first_c, rp, rc, rd, go);
         __syncthreads();  // the window is restaged by the next iteration
     };
 #pragma unroll 1

@@ -216,6 +216,12 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
     __syncthreads();
     const int nnb = ctl[1];
 
+    // the reference tap's own-cell term go_t * aref of the previous iteration, kept in a register
+    // instead of an LDS atomic (its float rounding differs from the fixed-point window's; the
+    // last iteration adds it to the window, which it flushes whole)
+    float refc[PX];
+#pragma unroll
+    for (int j = 0; j < PX; ++j) refc[j] = 0.f;
     int sh_prev = 0, t_abort = 0;
     for (int t = a.T; t >= 1 && !t_abort; --t) {
         const bool last = t == a.T;
@@ -245,7 +251,7 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
                 const float mine = ldexpf((float)(long long)gacc[(ly + R) * WW + lx + R], -sh_prev);
                 const float others = (exp_dbg(a.dbg) & 8u) ? 0.f
                                      : __hip_atomic_exchange(&gfr_p[cell], 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                gfr = mine + others;
+                gfr = (mine + others) + refc[j];
             }
             const float pt = pt_p[cell];
             float g = has_conf ? gfr * ce[j] : gfr;
@@ -291,8 +297,11 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
             if (own[j] < 0) continue;
             const int ly = own[j] >> 16, lx = own[j] & 0xffff;
             const int i = tid + j * NT;
-            if (exact) add_win((ly + R) * WW + lx + R, go[j] * aref[j]);  // reference tap: integer point, weight 1
-            else add_gl((y0 + ly) * W + x0 + lx, go[j] * aref[j]);
+            // reference tap: integer point, weight 1 (a register until the last iteration)
+            refc[j] = 0.f;
+            if (!exact) add_gl((y0 + ly) * W + x0 + lx, go[j] * aref[j]);
+            else if (t == 1) add_win((ly + R) * WW + lx + R, go[j] * aref[j]);
+            else refc[j] = go[j] * aref[j];
             const float4 a0 = reinterpret_cast<const float4 *>(avl)[2 * i], a1 = reinterpret_cast<const float4 *>(avl)[2 * i + 1];
             const float avj[K] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll

@@ -789,17 +789,11 @@ bool br_disabled() {
     return e && e[0] == '0';
 }
 
-// Pass 2 keeps conf' in an LDS window (bwd_coef_kernel CW); the experiments build only:
-// NLSPN_BWD_CW=0 stages it every iteration (A/B; read per call).
-bool bwd_coef_cw() {
-    if (!kExperiments) return true;
-    const char *e = getenv("NLSPN_BWD_CW");
-    return !(e && e[0] == '0');
-}
-
-size_t br_sync_offset_words(long long N, int K, long long tiles) {
-    const size_t w = (size_t)N * (3 + K) + (size_t)tiles;
-    return (w + kBrLine - 1) / kBrLine * kBrLine;  // a 128-B line boundary
+// The backward workspace: the two dL/df planes, then (from a 128-B line) the resident pass 1's
+// sync words — contiguous, so one memset clears both — then G (K planes), dL/dconf' and the
+// dL/dgamma partials.
+size_t br_sync_offset_words(long long N) {
+    return ((size_t)N * 2 + kBrLine - 1) / kBrLine * kBrLine;
 }
 
 // The whole section (see nlspn_propagate).  ev (optional, 2*T events): a dispatch-
@@ -1345,7 +1339,7 @@ size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw) {
     const size_t N = (size_t)B * H * W, K = (size_t)kh * kw - 1;
     // dL/df ping-pong, G = dL/daff - dL/daff_ref (K planes), dL/dconf', dL/dgamma partials, then
     // (line-aligned) the resident pass 1's sync words
-    return sizeof(float) * (br_sync_offset_words((long long)N, (int)K, bwd_tiles(B, H, W)) + kBrSyncWords);
+    return sizeof(float) * (br_sync_offset_words((long long)N) + kBrSyncWords + N * (K + 1) + (size_t)bwd_tiles(B, H, W));
 }
 
 int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -1379,17 +1373,16 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     hipStream_t s = as_stream(stream);
     float *ws = static_cast<float *>(workspace);
     float *gf[2] = {ws, ws + N};
-    float *g_aff = ws + 2 * N;
-    float *g_conf = ws + (2 + K) * N;
-    float *gpart = ws + (3 + K) * N;
+    unsigned *sync = reinterpret_cast<unsigned *>(ws) + br_sync_offset_words(N);
+    float *g_aff = ws + br_sync_offset_words(N) + kBrSyncWords;
+    float *g_conf = g_aff + K * N;
+    float *gpart = g_aff + (1 + K) * N;
     {
         BwdArgs probe{};
         probe.B = B; probe.H = H; probe.W = W;
         BwdLaunch L;
         if (int rc = select_bwd(probe, kh, kw, off_raw != nullptr, false, true, L)) return rc;
     }
-    // accumulators are initialised by step T; only step T's scatter target needs clearing
-    NLSPN_HIP_TRY(hipMemsetAsync(gf[(T - 1) & 1], 0, sizeof(float) * N, s));
     const bool vec = (W % 4 == 0) && aligned(pred_init, 16) && aligned(pred_inter, 16) && aligned(conf, 16) &&
                      aligned(conf_eff, 16) && aligned(dep, 16);
     const float *pi = static_cast<const float *>(pred_inter);
@@ -1415,9 +1408,6 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         int occ = 0;
         NLSPN_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBrNT, lds));
         if (occ < 1) return fail(NLSPN_EUNSUPPORTED, "resident backward: no room for a %d-thread part", kBrNT);
-        unsigned *sync = reinterpret_cast<unsigned *>(ws) + br_sync_offset_words(N, K, bwd_tiles(B, H, W));
-        NLSPN_HIP_TRY(hipMemsetAsync(gf[1], 0, sizeof(float) * N, s));  // (gf[(T-1)&1] is cleared above)
-        NLSPN_HIP_TRY(hipMemsetAsync(gf[0], 0, sizeof(float) * N, s));
         DevState *d = dev_state();
         for (int b0 = 0; b0 < B; b0 += bp.Bl) {
             const int nb = std::min(bp.Bl, B - b0);
@@ -1448,7 +1438,9 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
             }
             const unsigned grid = (unsigned)(nb * bp.py * bp.px);
             if (grid > (unsigned)device_cus() * (unsigned)occ) return fail(NLSPN_EUNSUPPORTED, "resident backward grid too large");
-            NLSPN_HIP_TRY(hipMemsetAsync(sync, 0, sizeof(unsigned) * kBrSyncWords, s));
+            // both dL/df planes and the sync words in one memset; later image groups: the sync words
+            if (b0 == 0) NLSPN_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(float) * (br_sync_offset_words(N) + kBrSyncWords), s));
+            else NLSPN_HIP_TRY(hipMemsetAsync(sync, 0, sizeof(unsigned) * kBrSyncWords, s));
             if ((rc = res_guard_before(s))) return rc;
             void *args[] = {&r};
             NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(kBrNT), args, (size_t)lds, s));
@@ -1456,6 +1448,8 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
             if ((rc = res_guard_after(s))) return rc;
         }
     }
+    // step launches: the accumulators are initialised by step T; only its scatter target needs clearing
+    if (!resident) NLSPN_HIP_TRY(hipMemsetAsync(gf[(T - 1) & 1], 0, sizeof(float) * N, s));
     for (int t = T; t >= 1 && !resident; --t) {
         const bool first = t == 1;
         BwdArgs a{};
@@ -1524,11 +1518,8 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         c.T = T;
         c.kind = kind;
         c.flags = flags;
-        const bool cw = bwd_coef_cw();
-        const void *fn = vec ? (cw ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4, true>)
-                                   : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4, false>))
-                             : (cw ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1, true>)
-                                   : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1, false>));
+        const void *fn = vec ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4>)
+                             : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1>);
         void *cargs[] = {&c};
         NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)bwd_tiles(B, H, W)), dim3(kBwdTH * kBwdTW), cargs, 0, s));
         if ((rc = check_launch("nlspn_propagate_backward coefficients"))) return rc;
