@@ -535,8 +535,13 @@ struct BwdCoefArgs {
 // staging both, profiles/r06/ab_bwd_resident_v1.json).  Issuing the next iteration's p loads
 // before the taps (one register window, 105 VGPRs; or capped at 5 waves, 9 VGPRs spilled)
 // measured 5 % / 2 % slower (profiles/r06/ab_bwd_pf_t18_rejected.json).
+// The coefficient sums contract into fused multiply-adds (the file is built with
+// -ffp-contract=off for the forward's exact IEEE sequence; the backward is checked to float
+// rounding, 1e-4 against the fp64 oracle and 1e-6 against the one-pass form): 0.4627 vs 0.4757
+// ms per C2 backward (profiles/r06/ab_bwd_pass2_fma.jsonl).
 template <int KH, int KW, int TH, int TW, int RY, int RX, int SV>
 __global__ void __launch_bounds__(TH * TW, NLSPN_BWD_COEF_WAVES) bwd_coef_kernel(BwdCoefArgs a) {
+#pragma clang fp contract(fast)
     constexpr int NT = TH * TW;
     constexpr int KK = KH * KW, REF = KK / 2, K = KK - 1;
     constexpr int PH = (KH - 1) / 2, PW = (KW - 1) / 2;
