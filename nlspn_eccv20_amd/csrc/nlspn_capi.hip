@@ -696,7 +696,8 @@ struct BwdLaunch {
     dim3 grid, block;
 };
 
-constexpr int kBwdTH = 8, kBwdTW = 32;  // backward tile (every geometry)
+constexpr int kBwdTH = 8, kBwdTW = 32;  // backward step tile (every geometry)
+constexpr int kBwdCoefTH = 16, kBwdCoefTW = 16;  // pass 2's tile: at most 2 x bwd_tiles() of them
 
 long long bwd_tiles(int B, int H, int W) {
     return (long long)B * ((H + kBwdTH - 1) / kBwdTH) * ((W + kBwdTW - 1) / kBwdTW);
@@ -1339,7 +1340,7 @@ size_t nlspn_backward_workspace_bytes(int B, int H, int W, int kh, int kw) {
     const size_t N = (size_t)B * H * W, K = (size_t)kh * kw - 1;
     // dL/df ping-pong, G = dL/daff - dL/daff_ref (K planes), dL/dconf', dL/dgamma partials, then
     // (line-aligned) the resident pass 1's sync words
-    return sizeof(float) * (br_sync_offset_words((long long)N) + kBrSyncWords + N * (K + 1) + (size_t)bwd_tiles(B, H, W));
+    return sizeof(float) * (br_sync_offset_words((long long)N) + kBrSyncWords + N * (K + 1) + 2 * (size_t)bwd_tiles(B, H, W));
 }
 
 int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, const void *conf,
@@ -1493,6 +1494,7 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         NLSPN_HIP_TRY(hipLaunchKernel(L.fn, L.grid, L.block, args, 0, s));
         if ((rc = check_launch("nlspn_propagate_backward step"))) return rc;
     }
+    int np_coef = 0;
     if (split) {
         BwdCoefArgs c{};
         c.pred_init = static_cast<const float *>(pred_init);
@@ -1513,15 +1515,19 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         c.gaff_bs = gaff_bs;
         c.N = N;
         c.B = B; c.H = H; c.W = W;
-        c.tiles_x = (W + kBwdTW - 1) / kBwdTW;
-        c.tiles_y = (H + kBwdTH - 1) / kBwdTH;
         c.T = T;
         c.kind = kind;
         c.flags = flags;
-        const void *fn = vec ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 4>)
-                             : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, kBwdTH, kBwdTW, 8, 8, 1>);
+        // 16 x 16 tiles: C2 0.4519 vs 0.4631 ms per backward against 8 x 32 (KITTI 0.941 vs 0.946;
+        // 16 x 32, 8 x 64, 4 x 64 and 4 x 32 slower or equal, profiles/r06/ab_bwd_coef_tile_*.json)
+        constexpr int cth = kBwdCoefTH, ctw = kBwdCoefTW;
+        const void *fn = vec ? reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, cth, ctw, 8, 8, 4>)
+                             : reinterpret_cast<const void *>(&bwd_coef_kernel<3, 3, cth, ctw, 8, 8, 1>);
+        c.tiles_x = (W + ctw - 1) / ctw;
+        c.tiles_y = (H + cth - 1) / cth;
+        np_coef = B * c.tiles_x * c.tiles_y;  // (<= 2 x bwd_tiles(): the partials' room)
         void *cargs[] = {&c};
-        NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)bwd_tiles(B, H, W)), dim3(kBwdTH * kBwdTW), cargs, 0, s));
+        NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)np_coef), dim3(cth * ctw), cargs, 0, s));
         if ((rc = check_launch("nlspn_propagate_backward coefficients"))) return rc;
     }
     const float *pinit = static_cast<const float *>(pred_init), *pdep = static_cast<const float *>(dep),
@@ -1531,7 +1537,7 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     float *gg = (grad_gamma && kind == NLSPN_AFF_TGASS) ? grad_gamma : nullptr;
     if (grad_gamma && !gg) NLSPN_HIP_TRY(hipMemsetAsync(grad_gamma, 0, sizeof(float), s));
     long long n_ = N;
-    int np = (int)bwd_tiles(B, H, W);
+    int np = split ? np_coef : (int)bwd_tiles(B, H, W);
     unsigned fl = flags;
     void *fargs[] = {&pinit, &pdep, &pconf, &pce, &gf0, &cg_conf, &gpi, &gc, &n_, &fl, &cgpart, &np, &gg};
     NLSPN_HIP_TRY(hipLaunchKernel(reinterpret_cast<const void *>(&bwd_final_kernel), dim3(elementwise_grid(N)),

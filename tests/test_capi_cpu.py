@@ -34,12 +34,12 @@ def test_abi_version_and_workspace():
     assert lib.nlspn_resident_config(0, 8, 228, 304, 3, 3, 18, 1, None, None, None) == 0  # no GPU here
     # backward: dL/df ping-pong, then (from a 128-B line) the resident pass 1's sync words (an
     # abort / registration line, one arrival line per part (up to 256) and an 8-word adjacency
-    # row per part), K planes of G, dL/dconf' and one dL/dgamma partial per 8x32 tile
+    # row per part), K planes of G, dL/dconf' and room for two dL/dgamma partials per 8x32 tile
     B, H, W, K = 8, 228, 304, 8
     tiles = B * ((H + 7) // 8) * ((W + 31) // 32)
     N = B * H * W
     gf = (2 * N + 31) // 32 * 32  # the two dL/df planes, line-aligned: the sync words follow them
-    assert lib.nlspn_backward_workspace_bytes(B, H, W, 3, 3) == 4 * (gf + 32 * 257 + 256 * 8 + N * (1 + K) + tiles)
+    assert lib.nlspn_backward_workspace_bytes(B, H, W, 3, 3) == 4 * (gf + 32 * 257 + 256 * 8 + N * (1 + K) + 2 * tiles)
     assert lib.nlspn_backward_workspace_bytes(0, H, W, 3, 3) == 0
     assert lib.nlspn_prop_step_backward_workspace_bytes(B, H, W) == 4 * 2 * B * H * W
     assert lib.nlspn_affinity_normalize_backward_workspace_bytes(B, K, H, W) > 0
