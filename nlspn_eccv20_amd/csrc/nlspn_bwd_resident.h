@@ -39,8 +39,9 @@
 //
 // Not bit-reproducible run to run (float atomics), like the step form and the reference's
 // col2im; equal to it to float rounding (tests/test_gpu_backward.py).  Every spin is bounded:
-// a timed-out wait raises the abort word and the device's sticky status word, and every part
-// fills the dL/dout planes it has not written with NaN before it exits.
+// a timed-out wait raises the abort word and the device's sticky status word; every part that
+// sees it (the word is global: parts of other images that spin long enough abort too) fills the
+// dL/dout planes it has not written, its dL/dconf' and its dL/df_0 cells with NaN before it exits.
 #pragma once
 
 #include "nlspn_backward.h"
@@ -79,7 +80,8 @@ struct BwdResArgs {
     int WH, WW;               // LDS window (PR + 2R) x (PC + 2R)
     unsigned flags;           // kPreserve (kAlwaysClip is not taken: the host keeps the step form)
     unsigned dbg;             // experiments build only (exp_dbg; results wrong on purpose): 1 no LDS
-                              // scatter, 2 no halo flush, 4 no waits, 8 no exchange read
+                              // scatter, 2 no halo flush, 4 no waits, 8 no exchange read, 16 part 0
+                              // aborts at its first wait (the abort path's test)
 };
 
 __device__ __forceinline__ unsigned br_load(const unsigned *p) {
@@ -227,6 +229,11 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
         const bool last = t == a.T;
         // ---- 1. wait for the neighbours' iteration t+1
         if (!last) {
+            if (tid == 0 && (exp_dbg(a.dbg) & 16u) && part == 0 && !ctl[0]) {  // test hook: raise the abort
+                __hip_atomic_store(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.status) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                ctl[0] = 1;
+            }
             if (tid == 0 && nnb > 0 && !ctl[0] && !(exp_dbg(a.dbg) & 4u))
                 if (!br_wait(sync, a.status, &sync[kBrLine * (1 + part)], (unsigned)nnb * (unsigned)(a.T - t))) ctl[0] = 1;
             __syncthreads();
@@ -370,6 +377,9 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
         if (own[j] < 0) continue;
         const int cell = (y0 + (own[j] >> 16)) * W + x0 + (own[j] & 0xffff);
         if (has_conf) a.g_conf[b * HW + cell] = t_abort ? __builtin_nanf("") : gcv[j];
+        // (and dL/df_0, which the final kernel turns into grad_pred_init: a memory-side store, the
+        // plane's other accesses in the launch being atomics)
+        if (t_abort) __hip_atomic_store(&gfb[0][cell], __builtin_nanf(""), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int t = t_abort; t >= 1; --t) {
             const int jgo = t - 1;
             float *go_p = jgo < 2 * K ? a.g_off + b * a.goff_bs + (size_t)jgo * HW

@@ -75,7 +75,50 @@ def general_path(B, H, W, sigma):
     print("ok general path taken", B, H, W, sigma)
 
 
+def bwd_abort(B, H, W, seed):
+    """The resident backward pass 1 aborting (NLSPN_BWD_RES_DBG=16: part 0 raises the abort at its
+    first wait): the device's sticky status raises; image 0's gradients hold NaN (its parts fill
+    the dL/dout, dL/dconf' and dL/df_0 cells they had not finished); the abort word is global, so
+    parts of other images that spin long enough abort too — every image's gradients are either
+    NaN-marked in all four tensors or equal to a clean call's, none silently wrong; the next call
+    runs clean."""
+    pi, dep, conf, aff, off, g = _inputs(B, H, W, seed=seed)
+
+    def grads(dbg):
+        if dbg is None:
+            os.environ.pop("NLSPN_BWD_RES_DBG", None)
+        else:
+            os.environ["NLSPN_BWD_RES_DBG"] = str(dbg)
+        leaves = [x.detach().clone().requires_grad_(True) for x in (pi, conf, aff, off, g)]
+        o = propagate(leaves[0], dep, leaves[1], leaves[2], leaves[3], leaves[4], prop_time=18)
+        o["pred"].sum().backward()
+        torch.cuda.synchronize()
+        os.environ.pop("NLSPN_BWD_RES_DBG", None)
+        return [x.grad for x in leaves]
+
+    ga = grads(16)
+    try:
+        _lib.check_resident()
+        raise AssertionError("the injected backward abort did not raise")
+    except RuntimeError as e:
+        assert "aborted" in str(e), e
+    gc = grads(None)
+    _lib.check_resident()
+    assert all(torch.isfinite(x).all() for x in gc)
+    rel = lambda x, y: float((x - y).norm() / y.norm())  # noqa: E731
+    aborted = []
+    for i in range(B):
+        nan = [bool(torch.isnan(x[i]).any()) for x in ga[:4]]
+        if i == 0 or any(nan):
+            assert all(nan), (i, nan)  # every gradient of an aborted image is marked
+            aborted.append(i)
+        else:
+            for x, y in zip(ga[:4], gc[:4]):
+                assert rel(x[i], y[i]) < 1e-6, (i, rel(x[i], y[i]))
+    print("ok bwd_abort", B, H, W, "aborted images", aborted)
+
+
 if __name__ == "__main__":
     assert "exp" in _lib.LIB_PATH, f"needs the experiments build, got {_lib.LIB_PATH}"
     case, args = sys.argv[1], [float(x) if "." in x else int(x) for x in sys.argv[2:]]
-    {"abort": abort, "general_path": general_path}[case](*args)
+    {"abort": abort, "general_path": general_path, "bwd_abort": bwd_abort}[case](*args)

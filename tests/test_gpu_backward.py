@@ -226,3 +226,20 @@ def test_resident_backward_equals_one_pass(monkeypatch, B, H, W, T, sigma):
     # (C2: ~5.5e5 terms; measured 1.9e-6 relative between the forms): its bar is 1e-5
     for k, bar in (("off_aff", 1e-6), ("pred_init", 1e-6), ("conf", 1e-6), ("gamma", 1e-5)):
         assert rel(res[k], one[k]) < bar, (k, rel(res[k], one[k]))
+
+
+def test_resident_backward_abort_raises_and_poisons():
+    """The resident pass 1's abort path (experiments build, child process; tests/_exp_cases.py
+    bwd_abort): the sticky status raises, the aborting image's gradients are NaN, the other
+    images' are intact, and the next call runs clean."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "nlspn_eccv20_amd", "lib", "exp", "libnlspn_hip_exp.so")
+    assert os.path.exists(lib), "experiments build missing: make -C nlspn_eccv20_amd/csrc exp"
+    env = dict(os.environ, NLSPN_LIB_PATH=lib)
+    env.pop("NLSPN_BWD_RES_DBG", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "tests", "_exp_cases.py"), "bwd_abort", "4", "228", "304", "7"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0 and "ok" in out.stdout, (out.stdout[-2000:], out.stderr[-3000:])
