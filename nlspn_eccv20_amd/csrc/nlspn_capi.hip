@@ -1399,8 +1399,12 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
     // Resident pass 1 (nlspn_bwd_resident.h): the two-pass form without the clamp's mask,
     // T >= 2, when every part of an image group fits on the device at once.
     BrPlan bp;
+    // Only when the whole batch fits one launch: with image groups in turn (KITTI B=4: two
+    // launches of two images) each group pays the setup and its own T-iteration chain, and the
+    // step launches measured faster (0.855 vs 0.938 ms per backward, profiles/r06/
+    // ab_bwd_two_parts_per_cu_kitti_rejected.json "steps" vs "nt1024").
     const bool resident = split && !(flags & NLSPN_ALWAYS_CLIP) && T >= 2 && !br_disabled() &&
-                          br_plan(B, H, W, device_cus(), bp);
+                          br_plan(B, H, W, device_cus(), bp) && bp.Bl >= B;
     if (resident) {
         const void *fn = reinterpret_cast<const void *>(&bwd_res_kernel<kBrPX>);
         const int WH = bp.PR + 2 * kBrR, WW = bp.PC + 2 * kBrR;
@@ -1410,8 +1414,7 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
         NLSPN_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBrNT, lds));
         if (occ < 1) return fail(NLSPN_EUNSUPPORTED, "resident backward: no room for a %d-thread part", kBrNT);
         DevState *d = dev_state();
-        for (int b0 = 0; b0 < B; b0 += bp.Bl) {
-            const int nb = std::min(bp.Bl, B - b0);
+        {  // the whole batch in one launch (bp.Bl == B)
             BwdResArgs r{};
             r.pred_inter = pi;
             r.conf_eff = conf ? static_cast<const float *>(conf_eff) : nullptr;
@@ -1430,18 +1433,17 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
             r.N = N;
             r.sync = sync;
             r.status = d ? d->dev_status : nullptr;
-            r.b0 = b0; r.H = H; r.W = W; r.T = T;
+            r.b0 = 0; r.H = H; r.W = W; r.T = T;
             r.py = bp.py; r.px = bp.px; r.PR = bp.PR; r.PC = bp.PC; r.WH = WH; r.WW = WW;
             r.flags = flags;
             if (kExperiments) {  // (A/B diagnostics, read per call)
                 const char *e = getenv("NLSPN_BWD_RES_DBG");
                 r.dbg = e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
             }
-            const unsigned grid = (unsigned)(nb * bp.py * bp.px);
+            const unsigned grid = (unsigned)(B * bp.py * bp.px);
             if (grid > (unsigned)device_cus() * (unsigned)occ) return fail(NLSPN_EUNSUPPORTED, "resident backward grid too large");
-            // both dL/df planes and the sync words in one memset; later image groups: the sync words
-            if (b0 == 0) NLSPN_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(float) * (br_sync_offset_words(N) + kBrSyncWords), s));
-            else NLSPN_HIP_TRY(hipMemsetAsync(sync, 0, sizeof(unsigned) * kBrSyncWords, s));
+            // both dL/df planes and the sync words in one memset
+            NLSPN_HIP_TRY(hipMemsetAsync(ws, 0, sizeof(float) * (br_sync_offset_words(N) + kBrSyncWords), s));
             if ((rc = res_guard_before(s))) return rc;
             void *args[] = {&r};
             NLSPN_HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(kBrNT), args, (size_t)lds, s));

@@ -209,7 +209,7 @@ def test_backward_long_section_one_pass_fallback(oracle):
 
 @pytest.mark.parametrize("B,H,W,T,sigma", [
     (8, 228, 304, 18, 2.0),   # C2: one launch, 4 x 8 parts of 57 x 38 per image
-    (4, 240, 1216, 18, 2.0),  # KITTI rows: two images per launch, two launches
+    (2, 240, 1216, 18, 2.0),  # KITTI rows: 128 parts of 60 x 38 per image (B = 4 takes the steps)
     (1, 228, 304, 6, 2.0),    # C1: 256 parts of one image
     (2, 40, 64, 12, 8.0),     # tiny parts, far taps: wide neighbour sets, footprints outside the window
     (3, 19, 45, 5, 2.0),      # parts of 1-2 rows, an odd image count
