@@ -213,6 +213,8 @@ def test_backward_long_section_one_pass_fallback(oracle):
     (1, 228, 304, 6, 2.0),    # C1: 256 parts of one image
     (2, 40, 64, 12, 8.0),     # tiny parts, far taps: wide neighbour sets, footprints outside the window
     (3, 19, 45, 5, 2.0),      # parts of 1-2 rows, an odd image count
+    (2, 48, 64, 2, 2.0),      # T = 2: one waited iteration
+    (2, 96, 128, 24, 2.0),    # T = 3K: every dL/dout plane of the gradient outputs in use
 ])
 def test_resident_backward_equals_one_pass(monkeypatch, B, H, W, T, sigma):
     """The resident pass 1 (nlspn_bwd_resident.h: iterations T..1 in one launch, neighbour-set
