@@ -75,7 +75,7 @@ struct BwdResArgs {
     long long goff_bs, gaff_bs, off_bs, N;
     unsigned *sync;           // kBrSyncWords, zero on entry
     unsigned *status;         // host-mapped sticky abort word of the device, or null
-    int b0, H, W, T;          // first image of this launch
+    int H, W, T;               // (the whole batch in one launch)
     int py, px, PR, PC;       // parts per image py x px, each PR x PC pixels
     int WH, WW;               // LDS window (PR + 2R) x (PC + 2R)
     unsigned flags;           // kPreserve (kAlwaysClip is not taken: the host keeps the step form)
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(kBrNT, 1) bwd_res_kernel(BwdResArgs a) {
     const int ppi = a.py * a.px;
     const int part = blockIdx.x;
     const int bl = part / ppi, pl = part - bl * ppi;
-    const int b = a.b0 + bl;
+    const int b = bl;
     const int pr = pl / a.px, pc = pl - pr * a.px;
     const int PR = a.PR, PC = a.PC, WH = a.WH, WW = a.WW, H = a.H, W = a.W;
     const int y0 = pr * PR, x0 = pc * PC, wy0 = y0 - R, wx0 = x0 - R;

@@ -1433,7 +1433,7 @@ int nlspn_propagate_backward(int dtype, const void *pred_init, const void *dep, 
             r.N = N;
             r.sync = sync;
             r.status = d ? d->dev_status : nullptr;
-            r.b0 = 0; r.H = H; r.W = W; r.T = T;
+            r.H = H; r.W = W; r.T = T;
             r.py = bp.py; r.px = bp.px; r.PR = bp.PR; r.PC = bp.PC; r.WH = WH; r.WW = WW;
             r.flags = flags;
             if (kExperiments) {  // (A/B diagnostics, read per call)
