@@ -147,7 +147,8 @@ __device__ __forceinline__ float aff_norm_backward(const float (&G)[K], const fl
 // registers and read-modify-write in chunks of 8 planes.
 // DIAG: diagnostic knobs for tools/bwd_bench (0 in the library; non-zero values
 // produce wrong gradients): 1 = no window flush, 4 = no accumulator read-modify-write,
-// 8 = no scatter at all (SPLIT: neither the LDS window adds nor the direct atomics).
+// 8 = no scatter at all (SPLIT: neither the LDS window adds nor the direct atomics), 16 = the
+// window adds as LDS f64 atomics (timing only: the flush still reads fixed point).
 // SPLIT (two-pass form, offsets): the step only produces dL/dout (written to go_out) and
 // scatters dL/df_{t-1}; the dL/daff and dL/doffset terms, which need f_{t-1} at every
 // tap, are computed for all T iterations afterwards by bwd_coef_kernel.  Without the
@@ -360,7 +361,10 @@ __global__ void __launch_bounds__(TH * TW) bwd_step_kernel(BwdArgs a) {
         //      and the col2im scatter of dL/df_{t-1} (.cuh:196-254)
         float *gfw = a.gf_write + b * HW;
         auto add_win = [&](int cell, float v) {
-            atomicAdd(&gacc[cell], (unsigned long long)__float2ll_rn(ldexpf(v, sh)));
+            if constexpr ((DIAG & 16) != 0)  // (tools/bwd_bench: LDS f64 atomic adds instead, timing only)
+                atomicAdd(reinterpret_cast<double *>(&gacc[cell]), (double)v);
+            else
+                atomicAdd(&gacc[cell], (unsigned long long)__float2ll_rn(ldexpf(v, sh)));
         };
         if (exact) add_win((ly + RY) * WW + lx + RX, go * aref);  // reference tap: integer point, weight 1
         else atomicAdd(&gfw[y * W + x], go * aref);

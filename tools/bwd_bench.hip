@@ -136,6 +136,8 @@ int main(int argc, char **argv) {
         mk<8, 32, 8, 0, true>("SPLIT 8x32 R8 (library)"),
         mk<8, 32, 8, 1, true>("SPLIT no-flush"),
         mk<8, 32, 8, 9, true>("SPLIT no-scatter"),
+        mk<8, 32, 8, 16, true>("SPLIT LDS f64 atomics"),
+        mk<8, 32, 8, 17, true>("SPLIT LDS f64 atomics no-flush"),
         {"SPLIT stream ceiling (32 planes)", reinterpret_cast<const void *>(&bwd_split_stream_ceiling), 0, 0},
     };
     const double bytes = 83.0 * 4 * N;
