@@ -413,6 +413,11 @@ int nlspn_resident_status(int clear);
 /* the narrow first encoder convs on the VALU: wpk is then the module's own (16, cin, 3, 3)
  * weight tensor (cin <= 16) and bias its own (16) */
 #define NLSPN_GC_S2_SMALL 6
+/* NLSPN_GC_S2 / NLSPN_GC_GRU2 on 32-pixel tiles (their co tile, hence their packed weights):
+ * nlspn_gconv switches to them by itself when 64-pixel tiles would give fewer than two
+ * workgroups per CU (the 1/8-scale layers at NYU B=8) */
+#define NLSPN_GC_S2_N32 23
+#define NLSPN_GC_GRU2_N32 24
 #define NLSPN_GC_ACT_NONE 0
 #define NLSPN_GC_ACT_RELU 1
 #define NLSPN_GC_ACT_TANH 2

@@ -1819,7 +1819,14 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     if (rows_of(a.npx) > p.xr)
         return fail(NLSPN_EUNSUPPORTED, "gconv: a tile of a %d-wide band spans more than %d window rows", a.bw, p.xr);
     a.tpb = (a.gh * a.bw + a.npx - 1) / a.npx;
-    const long long nwg = (long long)(p.mode == kGcT2 ? 4 : 1) * a.co_tiles * B * a.nbands * a.tpb;
+    long long nwg = (long long)(p.mode == kGcT2 ? 4 : 1) * a.co_tiles * B * a.nbands * a.tpb;
+    if (gru1) nwg = gc_gru1_wgs(a, p.wgco);  // (the qx workgroups take two pixel tiles each)
+    // Small grids: the same layer kind on 32-pixel tiles (the same co tile, hence the same packed
+    // weights) when 64-pixel tiles would leave most CUs one workgroup (NYU B=8: the 1/8-scale last
+    // encoder conv 104.1 -> 85.2 us, GRU2 52.6 -> 50.6 us; profiles/r06/gc_bench_layers_v4_n32.json)
+    if ((layer == NLSPN_GC_S2 || layer == NLSPN_GC_GRU2) && nwg < 2LL * device_cus())
+        return nlspn_gconv(layer == NLSPN_GC_S2 ? NLSPN_GC_S2_N32 : NLSPN_GC_GRU2_N32, x0, c0, x1, c1, wpk, bias, y, h,
+                           zb, rhb, qxb, hout, B, Hi, Wi, cout, ohs, ows, act, in_div, hc, stream);
     // (one image's channels of a source within a 32-bit buffer descriptor)
     if (nwg > 0x7fffffffLL || (long long)std::max(c0, c1) * Hi * Wi * 4 > 0x7fffffffLL)
         return fail(NLSPN_EINVAL, "gconv: problem too large");

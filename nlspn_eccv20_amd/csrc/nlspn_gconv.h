@@ -347,9 +347,35 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
     }
 }
 
+// GRU1's output-channel tiles differ in cost: z and r run K over h and x, qx over x alone (half).
+// One workgroup per (co tile, pixel tile) left the CUs unevenly loaded (every workgroup is
+// resident at once, so a CU's finish time is its summed work: 3.5 heavy-tile units on the most
+// loaded CUs against 2.8 on average).  A qx workgroup takes TWO consecutive pixel tiles instead,
+// so every workgroup costs the same.  (The pixel tiles of a GRU1 launch: gc_rest_count.)
+__host__ __device__ inline int gc_gru1_heavy_cots(const GconvArgs &a, int wgco) { return (2 * a.hc) / wgco; }
+__host__ __device__ inline int gc_rest_count(const GconvArgs &a) { return a.B * a.nbands * a.tpb; }
+__host__ __device__ inline int gc_gru1_wgs(const GconvArgs &a, int wgco) {
+    const int nh = gc_gru1_heavy_cots(a, wgco), nr = gc_rest_count(a);
+    return nh * nr + (a.co_tiles - nh) * ((nr + 1) / 2);
+}
+
 template <int MODE, int WM, int WN, int WGM, int WGN, int XR, int XP, int CC, int EPI>
 __global__ void __launch_bounds__(kGcNT) gconv_kernel(GconvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float gc_lds[];
+    if constexpr (EPI == kGcEpiGru1) {
+        using Cfg = GcCfg<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI>;
+        const int nh = gc_gru1_heavy_cots(a, Cfg::WGCO), nr = gc_rest_count(a);
+        const int wg = xcd_remap((int)blockIdx.x, gc_gru1_wgs(a, Cfg::WGCO));
+        if (wg < nh * nr) {  // z / r: one pixel tile
+            gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 0>(a, gc_lds, wg % nh + (wg / nh) * a.co_tiles);
+        } else {             // qx: two pixel tiles in turn
+            const int w = wg - nh * nr, nl = a.co_tiles - nh;
+            const int cot = nh + w % nl, r0 = 2 * (w / nl);
+            gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 0>(a, gc_lds, cot + r0 * a.co_tiles);
+            if (r0 + 1 < nr) gconv_body<MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI, 0>(a, gc_lds, cot + (r0 + 1) * a.co_tiles);
+        }
+        return;
+    }
     const int per_phase = a.co_tiles * a.B * a.nbands * a.tpb;
     const int nph = MODE == kGcT2 ? 4 : 1;
     const int wg = xcd_remap((int)blockIdx.x, per_phase * nph);  // neighbouring tiles (and co tiles) share an XCD
@@ -416,8 +442,9 @@ __global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float 
     }
 }
 
-// The instantiated configurations: X(id, MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI).  Ids 0..5 are the
-// presets NLSPN_GC_* of include/nlspn_prop.h; ids >= 16 are alternative tilings of the same
+// The instantiated configurations: X(id, MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI).  Ids 0..5, 23 and 24
+// are the presets NLSPN_GC_* of include/nlspn_prop.h (23 / 24: NLSPN_GC_S2 / NLSPN_GC_GRU2 on
+// 32-pixel tiles, which nlspn_gconv picks for small grids); the other ids >= 16 are alternative tilings of the same
 // layer kinds, selectable through nlspn_gconv's layer argument for A/B timing
 // (tools/gc_bench.py) and bit-compatible with the preset of their kind in layout (the packed
 // weights depend only on the kind's output-channel tile, which a variant must keep).
@@ -433,6 +460,8 @@ __global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float 
     X(18, kGcS1, 2, 4, 2, 2, 8, 40, 8, kGcEpiGru1)                 \
     X(20, kGcS2, 4, 1, 1, 4, 12, 40, 8, kGcEpiAct)                 \
     X(21, kGcT2, 4, 1, 1, 4, 6, 40, 4, kGcEpiAct)                  \
-    X(22, kGcT2, 1, 4, 1, 4, 6, 80, 4, kGcEpiAct)
+    X(22, kGcT2, 1, 4, 1, 4, 6, 80, 4, kGcEpiAct)                  \
+    X(23, kGcS2, 2, 1, 2, 2, 8, 40, 4, kGcEpiAct)                  \
+    X(24, kGcS1, 2, 1, 2, 2, 6, 40, 8, kGcEpiGru2)
 
 }  // namespace nlspn

@@ -16,8 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nlspn_eccv20_amd import NLSPNModel  # noqa: E402
 from nlspn_eccv20_amd import gru as G  # noqa: E402
 
-KINDS = {"s2": (G.GC_S2, [20]), "s2c16": (G.GC_S2_SMALL, []), "gru1": (G.GC_GRU1, [16, 18]),
-         "gru2": (G.GC_GRU2, [17]), "t2": (G.GC_T2, [21]), "t2c16": (G.GC_T2_C16, [22])}
+KINDS = {"s2": (G.GC_S2, [20, 23]), "s2c16": (G.GC_S2_SMALL, []), "gru1": (G.GC_GRU1, [16, 18]),
+         "gru2": (G.GC_GRU2, [17, 24]), "t2": (G.GC_T2, [21]), "t2c16": (G.GC_T2_C16, [22])}
 
 
 def main():
