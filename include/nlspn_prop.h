@@ -418,6 +418,9 @@ int nlspn_resident_status(int clear);
  * workgroups per CU (the 1/8-scale layers at NYU B=8) */
 #define NLSPN_GC_S2_N32 23
 #define NLSPN_GC_GRU2_N32 24
+/* NLSPN_GC_T2_C16 (its packed weights) with the affinity normalisation in its epilogue: the
+ * preset of nlspn_gconv_affnorm only (nlspn_gconv refuses it) */
+#define NLSPN_GC_T2_AFF 25
 #define NLSPN_GC_ACT_NONE 0
 #define NLSPN_GC_ACT_RELU 1
 #define NLSPN_GC_ACT_TANH 2
@@ -428,6 +431,18 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
                 const float *bias, float *y, const float *h, float *zb, float *rhb, float *qxb,
                 float *hout, int B, int Hi, int Wi, int cout, int ohs, int ows, int act,
                 float in_div, int hc, void *stream);
+/*
+ * decode_aff's last layer fused with the affinity normalisation that follows it
+ * (nlspnmodel.py:373 _aff_head, then :179-201 _affinity_normalization and :261-269
+ * _aff_insert at the next iteration's start; replaces nlspn_gconv(NLSPN_GC_T2_C16, ...)
+ * + nlspn_affinity_normalize): the K = 8 raw taps of the transposed conv (x0: (B, c0, Hi,
+ * Wi), weights packed as NLSPN_GC_T2_C16, act NLSPN_GC_ACT_*) are normalised per pixel as
+ * they leave the accumulators and stored as aff_out (B, K + 1, ohs, ows) with the reference
+ * tap at K / 2, kind NLSPN_AFF_*, *gamma the device scalar.  Bit-equal to the two launches.
+ */
+int nlspn_gconv_affnorm(const float *x0, int c0, const float *wpk, const float *bias, float *aff_out,
+                        const float *gamma, int kind, int B, int Hi, int Wi, int K, int ohs, int ows, int act,
+                        void *stream);
 
 #ifdef __cplusplus
 }

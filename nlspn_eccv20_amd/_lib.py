@@ -70,11 +70,13 @@ SIGNATURES = {
     "nlspn_gconv_pack_layout": (_i, [_i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "nlspn_gconv": (_i, [_i, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                          ctypes.c_float, _i, _vp]),
+    "nlspn_gconv_affnorm": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
 }
 
 # Entry points an A/B build (NLSPN_LIB_PATH) of an earlier round may lack; any other
 # missing symbol fails the load (a stale or wrong library is refused up front)
-AB_OPTIONAL = frozenset({"nlspn_resident_status", "nlspn_resident_config", "nlspn_gconv_pack_layout", "nlspn_gconv"})
+AB_OPTIONAL = frozenset({"nlspn_resident_status", "nlspn_resident_config", "nlspn_gconv_pack_layout", "nlspn_gconv",
+                         "nlspn_gconv_affnorm"})
 
 _lib = None
 

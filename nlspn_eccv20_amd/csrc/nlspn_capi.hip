@@ -1745,9 +1745,13 @@ int nlspn_gconv_pack_layout(int layer, int *co_tile, int *cin_chunk, int *transp
     return NLSPN_OK;
 }
 
-int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk, const float *bias,
-                float *y, const float *h, float *zb, float *rhb, float *qxb, float *hout, int B, int Hi, int Wi,
-                int cout, int ohs, int ows, int act, float in_div, int hc, void *stream) {
+}  // extern "C"
+namespace {
+// nlspn_gconv, and with gamma / aff_kind nlspn_gconv_affnorm (preset NLSPN_GC_T2_AFF)
+int gconv_impl(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk, const float *bias,
+               float *y, const float *h, float *zb, float *rhb, float *qxb, float *hout, int B, int Hi, int Wi,
+               int cout, int ohs, int ows, int act, float in_div, int hc, const float *gamma, int aff_kind,
+               void *stream) {
     if (layer == NLSPN_GC_S2_SMALL) {
         // (the kernel reads the module's own (16, cin, 3, 3) tensor)
         if (B < 1 || Hi < 1 || Wi < 1 || c0 < 1 || c1 != 0 || cout != 16 || c0 * 16 * 9 > kGsMaxW)
@@ -1776,7 +1780,12 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     // (the MFMA kernels stage their inputs by LDS-DMA, untouched: a divided input is the VALU
     // kernel's, NLSPN_GC_S2_SMALL)
     if (in_div != 1.f) return fail(NLSPN_EINVAL, "gconv: in_div %g needs the NLSPN_GC_S2_SMALL preset", (double)in_div);
-    const bool gru = p.epi != kGcEpiAct, gru1 = p.epi == kGcEpiGru1;
+    const bool gru = p.epi == kGcEpiGru1 || p.epi == kGcEpiGru2, gru1 = p.epi == kGcEpiGru1;
+    if ((p.epi == kGcEpiAff) != (gamma != nullptr))
+        return fail(NLSPN_EINVAL, "gconv: preset %d %s", layer,
+                    gamma ? "has no affinity epilogue" : "is nlspn_gconv_affnorm's (needs gamma)");
+    if (p.epi == kGcEpiAff && (cout != 8 || aff_kind < NLSPN_AFF_AS || aff_kind > NLSPN_AFF_TGASS))
+        return fail(NLSPN_EINVAL, "gconv affnorm: K = %d raw taps (supported 8), kind %d", cout, aff_kind);
     GconvArgs a{};
     a.x0 = x0; a.x1 = x1; a.w = wpk; a.bias = bias; a.y = y;
     a.h = h; a.zb = zb; a.rhb = rhb; a.qxb = qxb; a.hout = hout;
@@ -1794,6 +1803,8 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     a.act = act;
     a.in_div = in_div;
     a.hc = hc;
+    a.gamma = gamma;
+    a.aff_kind = aff_kind;
     if (gru) {
         if (hc < 1 || hc % p.wgco != 0 || !h || (gru1 ? (!zb || !rhb || !qxb || cout != 3 * hc || c0 != hc)
                                                                           : (!zb || !qxb || !hout || cout != hc || c1 != 0 || c0 != hc)))
@@ -1825,8 +1836,8 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     // weights) when 64-pixel tiles would leave most CUs one workgroup (NYU B=8: the 1/8-scale last
     // encoder conv 104.1 -> 85.2 us, GRU2 52.6 -> 50.6 us; profiles/r06/gc_bench_layers_v4_n32.json)
     if ((layer == NLSPN_GC_S2 || layer == NLSPN_GC_GRU2) && nwg < 2LL * device_cus())
-        return nlspn_gconv(layer == NLSPN_GC_S2 ? NLSPN_GC_S2_N32 : NLSPN_GC_GRU2_N32, x0, c0, x1, c1, wpk, bias, y, h,
-                           zb, rhb, qxb, hout, B, Hi, Wi, cout, ohs, ows, act, in_div, hc, stream);
+        return gconv_impl(layer == NLSPN_GC_S2 ? NLSPN_GC_S2_N32 : NLSPN_GC_GRU2_N32, x0, c0, x1, c1, wpk, bias, y, h,
+                          zb, rhb, qxb, hout, B, Hi, Wi, cout, ohs, ows, act, in_div, hc, nullptr, 0, stream);
     // (one image's channels of a source within a 32-bit buffer descriptor)
     if (nwg > 0x7fffffffLL || (long long)std::max(c0, c1) * Hi * Wi * 4 > 0x7fffffffLL)
         return fail(NLSPN_EINVAL, "gconv: problem too large");
@@ -1834,6 +1845,23 @@ int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, con
     void *args[] = {&a};
     NLSPN_HIP_TRY(hipLaunchKernel(p.fn, dim3((unsigned)nwg), dim3(kGcNT), args, (size_t)p.lds, as_stream(stream)));
     return check_launch("nlspn_gconv");
+}
+}  // namespace
+extern "C" {
+
+int nlspn_gconv(int layer, const float *x0, int c0, const float *x1, int c1, const float *wpk, const float *bias,
+                float *y, const float *h, float *zb, float *rhb, float *qxb, float *hout, int B, int Hi, int Wi,
+                int cout, int ohs, int ows, int act, float in_div, int hc, void *stream) {
+    return gconv_impl(layer, x0, c0, x1, c1, wpk, bias, y, h, zb, rhb, qxb, hout, B, Hi, Wi, cout, ohs, ows, act,
+                      in_div, hc, nullptr, 0, stream);
+}
+
+int nlspn_gconv_affnorm(const float *x0, int c0, const float *wpk, const float *bias, float *aff_out,
+                        const float *gamma, int kind, int B, int Hi, int Wi, int K, int ohs, int ows, int act,
+                        void *stream) {
+    if (!gamma || !aff_out) return fail(NLSPN_EINVAL, "gconv affnorm: null gamma or output");
+    return gconv_impl(NLSPN_GC_T2_AFF, x0, c0, nullptr, 0, wpk, bias, aff_out, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, B, Hi, Wi, K, ohs, ows, act, 1.f, 0, gamma, kind, stream);
 }
 
 int nlspn_resident_config(int dtype, int B, int H, int W, int kh, int kw, int T, int has_conf, int *grid,

@@ -35,7 +35,7 @@ namespace nlspn {
 constexpr int kGcNT = 256;  // threads per workgroup (4 waves)
 constexpr int kGcCP = 16;   // packed input channels: a multiple of this (every chunk size CC divides it)
 enum { kGcS1 = 0, kGcS2 = 1, kGcT2 = 2 };         // 3x3 pad 1 stride 1 / stride 2; transposed stride 2 (pad 1, output pad 1)
-enum { kGcEpiAct = 0, kGcEpiGru1 = 1, kGcEpiGru2 = 2 };
+enum { kGcEpiAct = 0, kGcEpiGru1 = 1, kGcEpiGru2 = 2, kGcEpiAff = 3 };
 enum { kGcActNone = 0, kGcActRelu = 1, kGcActTanh = 2 };
 
 struct GconvArgs {
@@ -57,6 +57,10 @@ struct GconvArgs {
     int act;               // kGcAct*
     float in_div;          // inputs divided by it (encode_dep: max_depth, :366): the VALU kernel only, 1 for the MFMA kernels
     int hc;                // GRU hidden channels
+    // kGcEpiAff (decode_aff's last layer, K = 8 raw taps): y is the normalised affinity with the
+    // reference tap inserted, (B, K + 1, ohs, ows), of kind aff_kind (kAff*) with *gamma
+    const float *gamma;
+    int aff_kind;
 };
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -323,6 +327,39 @@ __device__ __forceinline__ void gconv_body(const GconvArgs &a, float *lds, int w
                     else o = u;                                                    // convq's x half + bias
                     if (ok) dst[ob + (long long)(16 * m + 4 * lg + r) * HWo] = o;
                 }
+        } else if constexpr (EPI == kGcEpiAff) {
+            // _affinity_normalization + _aff_insert (nlspnmodel.py:179-201, :261-269) on the raw
+            // taps as they leave the accumulators: the same float values the two-kernel path
+            // stores and affnorm_kernel reloads, through the same normalize_taps, so bit-equal.
+            // Channels 0-3 sit in lane group 0, 4-7 in group 1 (same pixel, lane ^ 16): one
+            // exchange gives both groups all eight taps; group 0 stores planes 0-4, group 1 5-8.
+            static_assert(WM == 1 && WGM == 1, "kGcEpiAff: one 16-channel block holds the K = 8 taps");
+            float u[4], v[4], t[8][1], ref[1];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                u[r] = acc[0][n][r] + bv[0][r];
+                if (a.act == kGcActRelu) u[r] = u[r] < 0.f ? 0.f : u[r];
+                else if (a.act == kGcActTanh) u[r] = tanhf(u[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = __shfl_xor(u[r], 16, 64);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                t[r][0] = lg == 0 ? u[r] : v[r];
+                t[4 + r][0] = lg == 0 ? v[r] : u[r];
+            }
+            normalize_taps<8, 1>(t, ref, a.aff_kind, *a.gamma);
+            const long long HWs = (long long)a.ohs * a.ows;
+            const long long pixs = ok ? (long long)oy * a.ows + ox : 0;
+            float *yb = a.y + (long long)b * 9 * HWs + pixs;
+            if (ok && lg == 0) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) yb[c * HWs] = t[c][0];
+                yb[4 * HWs] = ref[0];
+            } else if (ok && lg == 1) {
+#pragma unroll
+                for (int c = 5; c < 9; ++c) yb[c * HWs] = t[c - 1][0];
+            }
         } else {  // kGcEpiGru2
             float qv[WM][4], zv[WM][4], hv[WM][4];
             const long long ob = ((long long)b * hc + co0) * HWo + pix;
@@ -444,7 +481,8 @@ __global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float 
 
 // The instantiated configurations: X(id, MODE, WM, WN, WGM, WGN, XR, XP, CC, EPI).  Ids 0..5, 23 and 24
 // are the presets NLSPN_GC_* of include/nlspn_prop.h (23 / 24: NLSPN_GC_S2 / NLSPN_GC_GRU2 on
-// 32-pixel tiles, which nlspn_gconv picks for small grids); the other ids >= 16 are alternative tilings of the same
+// 32-pixel tiles, which nlspn_gconv picks for small grids; 25: NLSPN_GC_T2_C16 with the affinity
+// normalisation in its epilogue, nlspn_gconv_affnorm); the other ids >= 16 are alternative tilings of the same
 // layer kinds, selectable through nlspn_gconv's layer argument for A/B timing
 // (tools/gc_bench.py) and bit-compatible with the preset of their kind in layout (the packed
 // weights depend only on the kind's output-channel tile, which a variant must keep).
@@ -462,6 +500,7 @@ __global__ void __launch_bounds__(kGsNT) gsmall_kernel(GconvArgs a, const float 
     X(21, kGcT2, 4, 1, 1, 4, 6, 40, 4, kGcEpiAct)                  \
     X(22, kGcT2, 1, 4, 1, 4, 6, 80, 4, kGcEpiAct)                  \
     X(23, kGcS2, 2, 1, 2, 2, 8, 40, 4, kGcEpiAct)                  \
-    X(24, kGcS1, 2, 1, 2, 2, 6, 40, 8, kGcEpiGru2)
+    X(24, kGcS1, 2, 1, 2, 2, 6, 40, 8, kGcEpiGru2)                 \
+    X(25, kGcT2, 1, 4, 1, 4, 6, 80, 8, kGcEpiAff)
 
 }  // namespace nlspn

@@ -11,7 +11,8 @@ iteration after the first,
 (``csrc/nlspn_gconv.h``): f32-input MFMA implicit GEMMs reading NCHW in place, bias and
 ReLU / Tanh / the GRU's sigmoid-tanh-blend in their epilogues, the crop written directly —
 9 launches per iteration where the module path issues ~40 (convolutions, bias adds, ReLUs,
-cats, sigmoids, tanh, blends, layout copies).  The 1- / 9-channel first encoder convs run on a
+cats, sigmoids, tanh, blends, layout copies), the last one also normalising the affinity
+(``nlspn_gconv_affnorm``: no separate normalisation launch).  The 1- / 9-channel first encoder convs run on a
 VALU kernel (as MFMA tiles their K would be mostly padding).  Numerics: exact f32 products and f32
 accumulation; only the summation order differs from MIOpen's (RMSE vs the reference's
 GRU-mode fixtures well inside their 1e-4 bar, tests/test_gpu_gru.py).
@@ -223,10 +224,24 @@ class GruConvs:
         self._run(P["gru2"], rh, hc, h=h, zb=z, qxb=qx, hout=hn, hc=hc)
         return hn
 
-    def decode_aff(self, P, h, crop):
-        """decode_aff + _clip_as (:228-250): the last layer stores only the cropped rows / columns."""
+    def decode_aff(self, P, h, crop, gamma=None, kind=None):
+        """decode_aff + _clip_as (:228-250): the last layer stores only the cropped rows / columns.
+        With ``gamma`` / ``kind`` (and K = 8 raw taps) the last layer also normalises them
+        (_affinity_normalization + _aff_insert, :179-201, :261-269) in its epilogue
+        (nlspn_gconv_affnorm): the (B, K+1, H, W) affinity, bit-equal to the conv followed by
+        ``affinity_normalization``, without the raw planes' round trip or a launch.  Otherwise
+        the raw (B, K, H, W) taps."""
         x = h
-        n = len(P["dec"])
-        for i, L in enumerate(P["dec"]):
-            x = self._convt(L, x, crop=crop if i == n - 1 else None)
-        return x
+        for L in P["dec"][:-1]:
+            x = self._convt(L, x)
+        L = P["dec"][-1]
+        if gamma is None or L.cout != 8 or L.layer != GC_T2_C16:
+            return self._convt(L, x, crop=crop)
+        B, _, Hi, Wi = x.shape
+        ohs, ows = (min(crop[0], 2 * Hi), min(crop[1], 2 * Wi)) if crop else (2 * Hi, 2 * Wi)
+        g = gamma.detach().reshape(-1)[:1].to(device=x.device, dtype=torch.float32).contiguous()
+        y = torch.empty((B, L.cout + 1, ohs, ows), device=x.device, dtype=torch.float32)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(_lib.get().nlspn_gconv_affnorm(_p(x), L.cin, _p(L.w), _p(L.b), _p(y), _p(g), _lib.AFF_KINDS[kind],
+                                                  B, Hi, Wi, L.cout, ohs, ows, L.act, stream))
+        return y

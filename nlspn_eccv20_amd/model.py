@@ -331,7 +331,11 @@ class NLSPNModel(nn.Module):
         """nlspnmodel.py:228-234 (+ the _clip_as crop :237-250)."""
         if self._native_gru(aff_feat):
             gc = self._gru_convs
-            aff = gc.decode_aff(gc.pack(self), aff_feat, (self.args.patch_height, self.args.patch_width))
+            # (K = 8: the last transposed conv normalises in its epilogue, nlspn_gconv_affnorm)
+            aff = gc.decode_aff(gc.pack(self), aff_feat, (self.args.patch_height, self.args.patch_width),
+                                gamma=self.aff_scale_const, kind=self.args.affinity)
+            if aff.shape[1] == self.num_neighbors + 1:
+                return aff
             return affinity_normalization(aff, self.aff_scale_const, self.args.affinity)
         aff = self.decode_aff(aff_feat)
         aff = aff[:, :, :self.args.patch_height, :self.args.patch_width].contiguous()

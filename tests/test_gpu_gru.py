@@ -87,3 +87,26 @@ def test_gru_mode_section_native_vs_modules():
     for a, b in zip(o["pred_inter"], r["pred_inter"]):
         assert float(torch.sqrt(torch.mean((a.double() - b.double()) ** 2))) <= 1e-4
     assert np.isfinite(o["pred"].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("kind", ["AS", "ASS", "TC", "TGASS"])
+@pytest.mark.parametrize("B,H,W", [(8, 228, 304), (1, 50, 70), (2, 17, 33)])
+def test_decode_aff_fused_normalisation_bitequal(kind, B, H, W):
+    """nlspn_gconv_affnorm (decode_aff's last transposed conv with the affinity normalisation
+    and the reference-tap insert in its epilogue, nlspnmodel.py:179-201, :261-269) against the
+    same conv storing the raw taps followed by nlspn_affinity_normalize: bit-equal, every plane,
+    crop included; and the raw taps' normalisation within the kernels' own check of the tap sum."""
+    from nlspn_eccv20_amd.propagation import affinity_normalization
+    m = _model(H, W, seed=11)
+    gc = GruConvs()
+    P = gc.pack(m)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    h = torch.randn((B, 128, (H + 7) // 8, (W + 7) // 8), device=DEV, generator=g)
+    gamma = torch.tensor([0.37], device=DEV)
+    with torch.no_grad():
+        raw = gc.decode_aff(P, h, (H, W))
+        ref = affinity_normalization(raw, gamma, kind)
+        fused = gc.decode_aff(P, h, (H, W), gamma=gamma, kind=kind)
+    assert fused.shape == (B, 9, H, W) == ref.shape
+    assert torch.equal(fused, ref), float((fused - ref).abs().max())
+    assert torch.allclose(fused.sum(1), torch.ones((B, H, W), device=DEV), atol=1e-5)
