@@ -413,7 +413,7 @@ def gru_section_timing(inputs, cfg, steps, dev):
                         "ms_per_step_graph_channels_last_tuned": round(tuned, 4)},
             "speedup_vs_tuned_modules": round(tuned / graph, 3), "steps": steps,
             "note": "per iteration: encode_dep, ConvGRU (hidden 128), decode_aff + crop as HIP f32-MFMA convolutions "
-                    "(gru.py; the first update also encode_aff), affinity normalisation, prop_step; graph = one "
+                    "(gru.py; the first update also encode_aff), the affinity normalisation in the last conv's epilogue (K = 8), prop_step; graph = one "
                     "hipGraph replay of the section (SectionGraph). modules: the same section on the torch modules "
                     "(MIOpen), default and channels_last + MIOpen algorithm search"}
 
